@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — STFT frames/s of the MI355X phase-vocoder hot path.
+
+Workload (BASELINE.json configs[2], the batched throughput configuration at the metric's
+N=1024 / hop=256): per GPU 1024 synthetic 44.1 kHz mono channels x 10 s (441 000
+samples, 1722 frames each), PV_STANDARD time-stretch 0.5 (out hop 128).  A "step" is one
+pass of the hot path (analysis -> phase processing -> resynthesis + overlap-add, libpv
+pv_process) over that batch, with the input resident in HBM.  Channels shard across
+ranks with no data-path collective (weak scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--no-cpu]
+  torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL)
+
+Rank 0 prints ONE JSON line (metric, value, roofline{...}, cpu_baseline{...}, ...).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "phase-vocoder_amd"))
+
+METRIC = "STFT frames/s @ N=1024,hop=256; % HBM roofline; RMS err vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SR = 44100
+
+
+def synth_channels(torch, C, n, seed0, device):
+    """configs 2-4 generator: 3 sines f~U[55,4000] Hz, a=0.1, random
+    phase, + U(+-1e-3) noise, seed = seed0 + channel.  Built on the device (plumbing)."""
+    t = torch.arange(n, dtype=torch.float64, device=device) / SR
+    x = torch.empty((C, n), dtype=torch.float32, device=device)
+    for c in range(C):
+        rng = np.random.default_rng(seed0 + c)
+        f = rng.uniform(55, 4000, 3)
+        ph = rng.uniform(0, 2 * np.pi, 3)
+        acc = torch.zeros(n, dtype=torch.float64, device=device)
+        for i in range(3):
+            acc += 0.1 * torch.sin(2 * np.pi * float(f[i]) * t + float(ph[i]))
+        g = torch.Generator(device=device).manual_seed(seed0 + c)
+        acc += (torch.rand(n, dtype=torch.float64, device=device, generator=g) * 2 - 1) * 1e-3
+        x[c] = acc.to(torch.float32)
+    return x
+
+
+def synth_channels_np(C, n, seed0):
+    t = np.arange(n) / SR
+    out = np.empty((C, n), np.float32)
+    for c in range(C):
+        rng = np.random.default_rng(seed0 + c)
+        f = rng.uniform(55, 4000, 3)
+        ph = rng.uniform(0, 2 * np.pi, 3)
+        acc = sum(0.1 * np.sin(2 * np.pi * f[i] * t + ph[i]) for i in range(3))
+        acc = acc + rng.uniform(-1e-3, 1e-3, n)
+        out[c] = acc.astype(np.float32)
+    return out
+
+
+def cpu_baseline(N, hop_div, effect, scale, n, target_s=10.0):
+    """The CPU oracle (oracle/pvref.c, OpenMP over channels) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pvref  # test infrastructure: used here only as the timed CPU baseline
+
+    threads = int(os.environ.get("PV_CPU_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    frames = pvref.num_frames(n, N // hop_div)
+    probe = synth_channels_np(threads, n, 20240)
+    t0 = time.perf_counter()
+    _, used = pvref.std_process_batch(probe, N, hop_div, effect, scale, frames, threads)
+    dt = time.perf_counter() - t0
+    rate = threads * frames / dt
+    C = max(threads, int(rate * target_s / frames) // threads * threads)
+    C = min(C, 1024)
+    xs = synth_channels_np(C, n, 20240)
+    t0 = time.perf_counter()
+    _, used = pvref.std_process_batch(xs, N, hop_div, effect, scale, frames, threads)
+    dt = time.perf_counter() - t0
+    return {"value": C * frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
+            "sample": f"{C} of the workload's channels x {n} samples ({C * frames} frames), "
+                      f"oracle/pvref.c fp32-contract analysis + fp64 synthesis, {dt:.1f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from pvamd import PhaseVocoder, STANDARD, TIME_SHIFT
+
+    N, hop_div, scale = 1024, 4, 0.5
+    n = int(round(args.seconds * SR))
+    C = args.channels
+    pv = PhaseVocoder(N, TIME_SHIFT, scale, hop_div, mode=STANDARD, max_channels=C,
+                      max_frames=pv_frames(n, N // hop_div), device=local)
+    frames = pv.num_frames(n)
+    x = synth_channels(torch, C, n, 20240 + rank * C, dev)
+    spec = pv.alloc_spec(C, frames)
+    out = pv.alloc_out(C, frames)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        pv.process(x, spec=spec, out=out)
+    torch.cuda.synchronize(dev)
+
+    pv.profile(True)
+    pv.profile_reset()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pv.process(x, spec=spec, out=out)
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    prof = pv.profile_read()
+    pv.profile(False)
+
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    total_frames = C * frames * world * args.steps
+    value = total_frames / dt
+
+    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time
+    hop_a, hop_s, B = N // hop_div, pv.outHopSize, N // 2 + 1
+    per_frame = {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
+                 "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
+                 "carry": 0, "runsum": 8 * B, "seam": 0}
+    dom = max(prof, key=lambda k: prof[k][0])
+    ms_tot, launches = prof[dom]
+    avg_ms = ms_tot / max(launches, 1)
+    alg_bytes = per_frame.get(dom, 0) * C * frames
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tj = json.load(open(args.traffic))
+            traffic = tj.get(dom, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}
+    path_bytes = (4 * hop_a + 4 * hop_s + 2 * 8 * B) * C * frames * world * args.steps
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(N, hop_div, ord("t"), scale, n)
+        except Exception as e:  # reported, never fatal for the GPU number
+            cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
+                   "sample": f"failed: {e}"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (3 sines U[55,4000] Hz a=0.1 + U(+-1e-3) noise, seed 20240+ch)",
+            "config": {"workload": "BASELINE configs[2]: 1024 mono ch x 10 s per GPU, N=1024 hop=256, "
+                                   "PV_STANDARD time-stretch 0.5",
+                       "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
+                       "out_hop": hop_s, "parallelism": f"channel-shard x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
+            "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def pv_frames(n, hop):
+    from pvamd import frame_count
+    return frame_count(n, hop)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * pv.h — C-ABI of the MI355X phase-vocoder hot path (libpv.so).
+ *
+ * Plain pointers and sizes only; every float / pv_float2 pointer handed to a compute
+ * entry point is a DEVICE pointer (hipMalloc / torch CUDA tensor) on the handle's device,
+ * and `stream` is a hipStream_t (NULL = the legacy default stream).  All calls are
+ * asynchronous with respect to the host (graph-capturable: no allocation, no sync).
+ *
+ * Which reference interface each entry point replaces (reference @ /root/reference):
+ *   pv_create        PhaseVocoder(int samples, Effect e, float scale, int hop)
+ *                      src/phaseVocoder.h:79-116  (window imp[], hop = samples/hop,
+ *                      outHopSize = scale*hop, cuFFT plans, streams)
+ *   pv_destroy       ~PhaseVocoder()  src/phaseVocoder.h:128-130; cufftDestroy main.cpp:396
+ *   pv_analysis      PhaseVocoder::analysis_CUFFT  src/phaseVocoder.cpp:25-33
+ *                      -> CudaPhase::pv_analysis_CUFFT  karnel/kernel.cu:299-348
+ *                      batched over channels x frames (main.cpp:228-250 loop)
+ *   pv_resynthesis   PhaseVocoder::resynthesis_CUFFT  src/phaseVocoder.cpp:60-76
+ *                      -> CudaPhase::resynthesis_CUFFT  karnel/kernel.cu:352-432
+ *                      batched, including the running overlap-add main.cpp:261-297
+ *   pv_process       analysis -> processing -> resynthesis fused pipeline (the offline
+ *                      loop of main.cpp:228-297 in one call); no reference counterpart
+ *   pv_frame_*       the hop/frame arithmetic of main.cpp:231 and main.cpp:266
+ *
+ * Errors: status codes instead of the reference's print-and-exit (io.cpp:115-124).  The
+ * header-only C++ drop-in (include/phaseVocoder.h) restores print-and-exit on top.
+ */
+#ifndef PV_H
+#define PV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PV_ABI_VERSION 1
+
+typedef struct pv_handle pv_handle;
+
+/* layout-compatible with HIP/CUDA float2 {x, y} (8 bytes, 8-byte aligned) */
+typedef struct pv_float2 {
+    float x, y;
+} pv_float2;
+
+typedef enum pv_status {
+    PV_OK = 0,
+    PV_ERR_ARG = 1,         /* invalid argument / size out of the handle's capacity */
+    PV_ERR_UNSUPPORTED = 2, /* configuration not supported (e.g. N not a power of 2) */
+    PV_ERR_HIP = 3,         /* HIP runtime error (pv_last_error() has the text)       */
+    PV_ERR_NOMEM = 4        /* device allocation failed                               */
+} pv_status;
+
+typedef enum pv_effect {
+    PV_TIME_SHIFT = 't',  /* phaseVocoder.h:6  */
+    PV_PITCH_SHIFT = 'p'  /* phaseVocoder.h:7  */
+} pv_effect;
+
+typedef enum pv_mode {
+    PV_MODE_REF_COMPAT = 0, /* the reference's active path, bugs included */
+    PV_MODE_STANDARD = 1    /* textbook phase vocoder (Hann, unwrap, true frequency)     */
+} pv_mode;
+
+typedef struct pv_config {
+    int n_samps;      /* N, window length: power of 2; STANDARD 256..4096, REF_COMPAT 128..2048 */
+    int hop_div;      /* hop = N / hop_div (phaseVocoder.h:79 4th argument is a divisor)  */
+    int effect;       /* pv_effect                                                      */
+    float scale;      /* TIME_SHIFT: out_hop = (int)(scale*hop); PITCH_SHIFT: pitch ratio */
+    int mode;         /* pv_mode                                                        */
+    int max_channels; /* workspace capacity                                             */
+    int max_frames;   /* workspace capacity, frames per channel                          */
+    int device;       /* HIP device ordinal                                             */
+} pv_config;
+
+typedef struct pv_info {
+    int n_samps, hop, out_hop;
+    int spec_bins;      /* bins written per frame: N/2+1 (STANDARD) or 2N (REF_COMPAT)  */
+    int spec_stride;    /* pv_float2 elements between consecutive frames of a channel   */
+    int frames_per_run; /* frames per workgroup run                      */
+    int mode, effect;
+    float scale;
+} pv_info;
+
+int pv_abi_version(void);
+const char* pv_status_string(pv_status s);
+const char* pv_last_error(void); /* thread-local text of the last failure */
+
+pv_status pv_create(const pv_config* cfg, pv_handle** out);
+void pv_destroy(pv_handle* h);
+pv_status pv_get_info(const pv_handle* h, pv_info* info);
+
+/* main.cpp:231 — analysis frames of an n-sample channel: ceil((n - hop)/hop), >= 0 */
+int pv_frame_count(long long n_samples, int hop);
+/* samples of the full overlap-add of `frames` frames: frames*out_hop + N - out_hop */
+long long pv_output_length(const pv_handle* h, int frames);
+
+/* Analysis of `frames` frames per channel.  Frame t of channel c reads
+ * x[c*ldx + t*hop + i], i < N; samples at index >= n_samples read as 0.
+ * spec[c*ld_spec + t*spec_stride + k] = {magnitude, phase}, k < spec_bins. */
+pv_status pv_analysis(pv_handle* h, const float* x, long long ldx, long long n_samples,
+                      int channels, int frames, pv_float2* spec, long long ld_spec, void* stream);
+
+/* Processing + resynthesis of `frames` analysed frames per channel (spec is read only).
+ * out[c*ldo + i], i < pv_output_length(h, frames): the full overlap-add.  ola_in
+ * (nullable) holds N - out_hop samples per channel (stride ld_ola) already accumulated
+ * at the start of this block (the reference's backFrame tail). */
+pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                         int frames, const float* ola_in, long long ld_ola, float* out,
+                         long long ldo, void* stream);
+
+/* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer). */
+pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
+                     int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
+                     long long ldo, void* stream);
+
+/* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py). */
+pv_status pv_profile_enable(pv_handle* h, int enable);
+/* names[i] (static strings), total ms and launch count of each kernel since the last
+ * reset; returns number of kernels written (<= cap). Synchronises the recorded events. */
+int pv_profile_read(pv_handle* h, const char** names, double* total_ms, int* launches, int cap);
+void pv_profile_reset(pv_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PV_H */

@@ -1,0 +1,579 @@
+// pv_api.cpp — host side of libpv: the C-ABI declared in include/pv.h.
+//
+// Owns the per-handle constant tables (windows, twiddles, unwrap tables, pitch map),
+// the workspace (run sums, carries, overlap tails) and the launch sequence of the
+// pipeline.  No allocation or synchronisation happens inside the compute
+// entry points, so a caller may capture them into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pv.h"
+#include "pv_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+pv_status fail(pv_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define PV_HIP(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(e_ == hipErrorOutOfMemory ? PV_ERR_NOMEM : PV_ERR_HIP,          \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));             \
+    } while (0)
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr int kNumKernels = 6;
+const char* kKernelNames[kNumKernels] = {"analysis", "runsum", "carry",
+                                         "synthesis", "seam", "compat_analysis"};
+enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5 };
+
+bool is_pow2(long long v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// ---- table recipes (identical double -> float formulas to the oracle, pvref.c) ----
+void hann_periodic(int N, std::vector<float>& w) {
+    w.resize(N);
+    for (int n = 0; n < N; ++n)
+        w[n] = (float)(0.5 - 0.5 * std::cos(2.0 * kPi * (double)n / (double)N));
+}
+
+void hamming_ref(int N, std::vector<float>& w) {
+    // phaseVocoder.h:85-89
+    w.resize(N);
+    float omega = (float)(2.0 * kPi / (double)(N - 1));
+    for (int i = 0; i < N; ++i) {
+        float arg = omega * (float)i;
+        w[i] = 0.54f - 0.46f * cosf(arg);
+    }
+}
+
+float2 tw_entry(long long m, long long L) {
+    double a = 2.0 * kPi * (double)m / (double)L;
+    return make_float2((float)std::cos(a), (float)(-std::sin(a)));
+}
+
+// stage-major table for an L-point Stockham FFT: stage Ns at [Ns-1, 2Ns-1)
+void stage_twiddles(int L, std::vector<float2>& t) {
+    t.assign(L, make_float2(0.f, 0.f));
+    for (int Ns = 1; Ns < L; Ns <<= 1)
+        for (int idx = 0; idx < Ns; ++idx) t[Ns - 1 + idx] = tw_entry((long long)idx * (L / (2 * Ns)), L);
+}
+
+void split_twiddles(int N, std::vector<float2>& t) {
+    t.resize(N / 2 + 1);
+    for (int k = 0; k <= N / 2; ++k) t[k] = tw_entry(k, N);
+}
+
+struct Profile {
+    bool enabled = false;
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    std::vector<int> ev_kernel;
+    double total_ms[kNumKernels] = {0};
+    int launches[kNumKernels] = {0};
+};
+
+}  // namespace
+
+struct pv_handle {
+    pv_config cfg{};
+    int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
+    int spec_bins = 0, spec_stride = 0, F = 16, ring = 0, tail_len = 0, max_runs = 0;
+    int mode = 0, effect = 0, pitch = 0, aligned_hop = 1;
+    float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
+    unsigned long long p_mod = 0, q = 1;
+    int q_pow2 = 1;
+    // device tables
+    float *d_win = nullptr, *d_gain = nullptr, *d_ek = nullptr;
+    float2 *d_tw_ana = nullptr, *d_tws_ana = nullptr, *d_tw_syn = nullptr, *d_tws_syn = nullptr;
+    unsigned* d_jk_mod = nullptr;
+    int *d_src_first = nullptr, *d_src_cnt = nullptr;
+    // workspace
+    int *d_runsum = nullptr, *d_carry = nullptr;
+    float* d_tails = nullptr;
+    Profile prof;
+};
+
+namespace {
+
+template <typename T>
+pv_status upload(T** dst, const std::vector<T>& src) {
+    PV_HIP(hipMalloc((void**)dst, sizeof(T) * (src.empty() ? 1 : src.size())));
+    if (!src.empty()) PV_HIP(hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+    return PV_OK;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+pv_status prof_begin(pv_handle* h, int kernel, hipStream_t s) {
+    if (!h->prof.enabled) return PV_OK;
+    hipEvent_t a, b;
+    PV_HIP(hipEventCreate(&a));
+    PV_HIP(hipEventCreate(&b));
+    PV_HIP(hipEventRecord(a, s));
+    h->prof.ev_start.push_back(a);
+    h->prof.ev_stop.push_back(b);
+    h->prof.ev_kernel.push_back(kernel);
+    return PV_OK;
+}
+
+pv_status prof_end(pv_handle* h, hipStream_t s) {
+    if (!h->prof.enabled) return PV_OK;
+    PV_HIP(hipEventRecord(h->prof.ev_stop.back(), s));
+    return PV_OK;
+}
+
+#define PV_LAUNCH(h, kid, s, call)                                                    \
+    do {                                                                              \
+        pv_status st_ = prof_begin(h, kid, s);                                        \
+        if (st_ != PV_OK) return st_;                                                 \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(PV_ERR_HIP, std::string(kKernelNames[kid]) + " launch: " +    \
+                                        hipGetErrorString(e_));                       \
+        st_ = prof_end(h, s);                                                         \
+        if (st_ != PV_OK) return st_;                                                 \
+    } while (0)
+
+int nruns_of(const pv_handle* h, int frames) { return (frames + h->F - 1) / h->F; }
+
+pv_status check_common(const pv_handle* h, int channels, int frames) {
+    if (!h) return fail(PV_ERR_ARG, "null handle");
+    if (channels < 0 || frames < 0) return fail(PV_ERR_ARG, "negative channels/frames");
+    if (channels > h->cfg.max_channels || frames > h->cfg.max_frames)
+        return fail(PV_ERR_ARG, "channels/frames exceed the handle's capacity (max_channels, max_frames)");
+    return PV_OK;
+}
+
+pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, int C, int frames,
+                      pv_float2* spec, long long ld_spec, bool want_runsum, hipStream_t s) {
+    if (C == 0 || frames == 0) return PV_OK;
+    if (!x || !spec) return fail(PV_ERR_ARG, "null x/spec");
+    if (ld_spec < (long long)frames * h->spec_stride)
+        return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
+    if (C > 1 && ldx < n) return fail(PV_ERR_ARG, "ldx < n_samples");
+    pv::AnaParams p{};
+    p.x = x;
+    p.ldx = ldx;
+    p.n = n;
+    p.hop = h->hop;
+    p.frames = frames;
+    p.F = h->F;
+    p.nruns = nruns_of(h, frames);
+    p.aligned = (((uintptr_t)x & 7) == 0) && (ldx % 2 == 0) && (h->hop % 2 == 0);
+    p.win = h->d_win;
+    p.tw = h->d_tw_ana;
+    p.tws = h->d_tws_ana;
+    p.ek = h->d_ek;
+    p.spec = reinterpret_cast<float2*>(spec);
+    p.ld_spec = ld_spec;
+    p.spec_stride = h->spec_stride;
+    p.runsum = want_runsum ? h->d_runsum : nullptr;
+    p.bins_pad = h->bins_pad;
+    p.nan_faithful = 0;
+    if (h->mode == PV_MODE_STANDARD)
+        PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
+    else
+        PV_LAUNCH(h, KCA, s, pv::launch_compat_analysis(h->L_ana, C, p, s));
+    return PV_OK;
+}
+
+pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int C, int frames,
+                         const float* ola_in, long long ld_ola, float* out, long long ldo,
+                         bool have_runsum, hipStream_t s) {
+    if (C == 0 || frames == 0) {
+        return PV_OK;
+    }
+    if (!spec || !out) return fail(PV_ERR_ARG, "null spec/out");
+    const long long olen = pv_output_length(h, frames);
+    if (C > 1 && ldo < olen) return fail(PV_ERR_ARG, "ldo < pv_output_length");
+    if (ld_spec < (long long)frames * h->spec_stride)
+        return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
+    const int nruns = nruns_of(h, frames);
+    const float2* sp = reinterpret_cast<const float2*>(spec);
+    if (h->mode == PV_MODE_STANDARD) {
+        pv::ScanParams sc{};
+        sc.spec = sp;
+        sc.ld_spec = ld_spec;
+        sc.spec_stride = h->spec_stride;
+        sc.frames = frames;
+        sc.F = h->F;
+        sc.nruns = nruns;
+        sc.L = h->L_syn;
+        sc.bins_pad = h->bins_pad;
+        sc.ek = h->d_ek;
+        sc.runsum = h->d_runsum;
+        sc.carry = h->d_carry;
+        if (!have_runsum) PV_LAUNCH(h, KRS, s, pv::launch_runsum(C, sc, s));
+        PV_LAUNCH(h, KC, s, pv::launch_carry(C, sc, s));
+    }
+    pv::SynParams p{};
+    p.spec = sp;
+    p.ld_spec = ld_spec;
+    p.spec_stride = h->spec_stride;
+    p.frames = frames;
+    p.F = h->F;
+    p.nruns = nruns;
+    p.bins_pad = h->bins_pad;
+    p.carry = h->d_carry;
+    p.ek = h->d_ek;
+    p.jk_mod = h->d_jk_mod;
+    p.src_first = h->d_src_first;
+    p.src_cnt = h->d_src_cnt;
+    p.pitch = h->pitch;
+    p.rho = h->rho;
+    p.p_mod = h->p_mod;
+    p.q = h->q;
+    p.q_pow2 = h->q_pow2;
+    p.inv_q = h->inv_q;
+    p.tw = h->d_tw_syn;
+    p.tws = h->d_tws_syn;
+    p.gain = h->d_gain;
+    p.rot = (h->mode == PV_MODE_REF_COMPAT) ? h->N / 2 : 0;
+    p.hs = h->hs;
+    p.ring_size = h->ring;
+    p.out = out;
+    p.ldo = ldo;
+    p.out_len = olen;
+    p.tails = h->d_tails;
+    p.tail_len = h->tail_len;
+    PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, h->mode == PV_MODE_STANDARD ? 0 : 1, C, p, s));
+    if (nruns > 1 || ola_in != nullptr) {
+        pv::SeamParams sm{};
+        sm.out = out;
+        sm.ldo = ldo;
+        sm.out_len = olen;
+        sm.tails = h->d_tails;
+        sm.ola_in = ola_in;
+        sm.ld_ola = ld_ola;
+        sm.nruns = nruns;
+        sm.F = h->F;
+        sm.hs = h->hs;
+        sm.tail_len = h->tail_len;
+        PV_LAUNCH(h, KSEAM, s, pv::launch_seam(C, sm, s));
+    }
+    return PV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pv_abi_version(void) { return PV_ABI_VERSION; }
+
+const char* pv_status_string(pv_status s) {
+    switch (s) {
+        case PV_OK: return "PV_OK";
+        case PV_ERR_ARG: return "PV_ERR_ARG";
+        case PV_ERR_UNSUPPORTED: return "PV_ERR_UNSUPPORTED";
+        case PV_ERR_HIP: return "PV_ERR_HIP";
+        case PV_ERR_NOMEM: return "PV_ERR_NOMEM";
+    }
+    return "PV_ERR_UNKNOWN";
+}
+
+const char* pv_last_error(void) { return g_last_error.c_str(); }
+
+int pv_frame_count(long long n_samples, int hop) {
+    // main.cpp:231: for (i = 0; i < numSamples - hopSize; i += hopSize)
+    if (hop <= 0) return 0;
+    long long span = n_samples - hop;
+    if (span <= 0) return 0;
+    return (int)((span + hop - 1) / hop);
+}
+
+long long pv_output_length(const pv_handle* h, int frames) {
+    if (!h || frames <= 0) return 0;
+    return (long long)frames * h->hs + (h->N - h->hs);
+}
+
+pv_status pv_get_info(const pv_handle* h, pv_info* info) {
+    if (!h || !info) return fail(PV_ERR_ARG, "null argument");
+    info->n_samps = h->N;
+    info->hop = h->hop;
+    info->out_hop = h->hs;
+    info->spec_bins = h->spec_bins;
+    info->spec_stride = h->spec_stride;
+    info->frames_per_run = h->F;
+    info->mode = h->mode;
+    info->effect = h->effect;
+    info->scale = h->scale;
+    return PV_OK;
+}
+
+void pv_destroy(pv_handle* h) {
+    if (!h) return;
+    DeviceGuard g(h->cfg.device);
+    void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
+                    h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
+                    h->d_carry, h->d_tails};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
+    for (auto e : h->prof.ev_stop) (void)hipEventDestroy(e);
+    delete h;
+}
+
+pv_status pv_create(const pv_config* cfg, pv_handle** out) {
+    if (!cfg || !out) return fail(PV_ERR_ARG, "null argument");
+    *out = nullptr;
+    const int N = cfg->n_samps;
+    if (!is_pow2(N)) return fail(PV_ERR_UNSUPPORTED, "n_samps must be a power of two");
+    if (cfg->mode != PV_MODE_STANDARD && cfg->mode != PV_MODE_REF_COMPAT)
+        return fail(PV_ERR_ARG, "unknown mode");
+    if (cfg->effect != PV_TIME_SHIFT && cfg->effect != PV_PITCH_SHIFT)
+        return fail(PV_ERR_ARG, "unknown effect");
+    if (cfg->hop_div <= 0 || N / cfg->hop_div <= 0) return fail(PV_ERR_ARG, "bad hop_div");
+    if (cfg->max_channels < 0 || cfg->max_frames < 0) return fail(PV_ERR_ARG, "negative capacity");
+    if (!(cfg->scale > 0.0f) || !std::isfinite(cfg->scale)) return fail(PV_ERR_ARG, "scale must be > 0");
+    if (cfg->mode == PV_MODE_STANDARD && (N < 256 || N > 4096))
+        return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: n_samps in [256, 4096]");
+    if (cfg->mode == PV_MODE_REF_COMPAT && (N < 256 || N > 2048))
+        return fail(PV_ERR_UNSUPPORTED, "REF_COMPAT mode: n_samps in [256, 2048]");
+
+    pv_handle* h = new pv_handle();
+    h->cfg = *cfg;
+    h->N = N;
+    h->mode = cfg->mode;
+    h->effect = cfg->effect;
+    h->scale = cfg->scale;
+    h->hop = N / cfg->hop_div;  // phaseVocoder.h:79
+    if (cfg->effect == PV_TIME_SHIFT) {
+        float f = cfg->scale * (float)h->hop;  // phaseVocoder.h:104 (float -> int)
+        h->hs = (int)f;
+    } else {
+        h->hs = h->hop;  // PITCH_SHIFT: defined by the build (reference leaves it unset)
+    }
+    if (h->hs <= 0 || h->hs > N) {
+        delete h;
+        return fail(PV_ERR_UNSUPPORTED, "out hop must be in [1, N]");
+    }
+    if (h->mode == PV_MODE_REF_COMPAT && cfg->effect == PV_PITCH_SHIFT && cfg->scale != 1.0f) {
+        delete h;
+        return fail(PV_ERR_UNSUPPORTED, "REF_COMPAT implements no pitch shift (phaseVocoder.h:107-110)");
+    }
+    if (h->mode == PV_MODE_REF_COMPAT && cfg->effect == PV_TIME_SHIFT && h->hs != h->hop) {
+        // kernel.cu:354 hard-codes timeScale = 1: the reference only changes the OLA hop.
+    }
+    h->pitch = (cfg->mode == PV_MODE_STANDARD && cfg->effect == PV_PITCH_SHIFT) ? 1 : 0;
+    h->L_syn = N / 2;
+    h->L_ana = (h->mode == PV_MODE_STANDARD) ? N / 2 : N;
+    h->bins = N / 2 + 1;
+    h->bins_pad = (h->bins + 7) & ~7;
+    h->spec_bins = (h->mode == PV_MODE_STANDARD) ? h->bins : 2 * N;
+    h->spec_stride = (h->spec_bins + 7) & ~7;
+    if (h->L_ana > 2048 || h->L_syn > 2048 || h->L_syn < 128) {
+        delete h;
+        return fail(PV_ERR_UNSUPPORTED, "FFT length outside [128, 2048]");
+    }
+    h->tail_len = N - h->hs;
+    // frames per run: multiple of 4 (one round = 4 waves), run span >= overlap tail
+    int F = 16;
+    while ((long long)F * h->hs < h->tail_len) F += 4;
+    h->F = F;
+    int ring = 1;
+    while (ring < 4 * h->hs + N) ring <<= 1;
+    h->ring = ring;
+    h->max_runs = (cfg->max_frames + F - 1) / F;
+
+    DeviceGuard g(cfg->device);
+    pv_status st = PV_OK;
+    auto bail = [&](pv_status s) {
+        pv_destroy(h);
+        return s;
+    };
+
+    // ---- windows and gains
+    std::vector<float> win, gain(N);
+    if (h->mode == PV_MODE_STANDARD) {
+        hann_periodic(N, win);
+        double sw2 = 0.0;
+        std::vector<double> wd(N);
+        for (int i = 0; i < N; ++i) {
+            wd[i] = 0.5 - 0.5 * std::cos(2.0 * kPi * (double)i / (double)N);
+            sw2 += wd[i] * wd[i];
+        }
+        for (int i = 0; i < N; ++i) gain[i] = (float)(wd[i] * ((double)h->hs / sw2) / (double)N);
+    } else {
+        hamming_ref(N, win);
+        for (int i = 0; i < N; ++i) gain[i] = win[i] / (float)N;  // kernel.cu:380 /N, :406 window
+    }
+    if ((st = upload(&h->d_win, win)) != PV_OK) return bail(st);
+    if ((st = upload(&h->d_gain, gain)) != PV_OK) return bail(st);
+
+    // ---- twiddles
+    std::vector<float2> t;
+    stage_twiddles(h->L_ana, t);
+    if ((st = upload(&h->d_tw_ana, t)) != PV_OK) return bail(st);
+    split_twiddles(2 * h->L_ana, t);
+    if ((st = upload(&h->d_tws_ana, t)) != PV_OK) return bail(st);
+    stage_twiddles(h->L_syn, t);
+    if ((st = upload(&h->d_tw_syn, t)) != PV_OK) return bail(st);
+    split_twiddles(N, t);
+    if ((st = upload(&h->d_tws_syn, t)) != PV_OK) return bail(st);
+
+    // ---- unwrap tables and the rational output-phase factor rho = p/q
+    const int B = h->bins;
+    std::vector<float> ek(B);
+    std::vector<long long> jk(B);
+    for (int k = 0; k < B; ++k) {
+        long long kh = (long long)k * h->hop;
+        long long r = kh % N;
+        long long rr = (r > N / 2) ? r - N : r;
+        ek[k] = (float)(2.0 * kPi * (double)rr / (double)N);
+        jk[k] = (kh - rr) / N;
+    }
+    unsigned long long pn = 1, qd = 1;
+    if (h->pitch) {
+        int e2 = 0;
+        double m = std::frexp((double)cfg->scale, &e2);  // scale = m * 2^e2, m in [0.5,1)
+        long long mant = (long long)std::ldexp(m, 24);   // exact: float has 24 bits
+        int ex = e2 - 24;
+        while ((mant & 1) == 0 && ex < 0) { mant >>= 1; ++ex; }
+        if (ex >= 0) { pn = (unsigned long long)mant << ex; qd = 1; }
+        else { pn = (unsigned long long)mant; qd = 1ull << (-ex); }
+        h->rho = cfg->scale;
+    } else {
+        long long a = h->hs, b = h->hop;
+        long long x = a, y = b;
+        while (y) { long long tt = x % y; x = y; y = tt; }
+        pn = a / x;
+        qd = b / x;
+        h->rho = (float)((double)h->hs / (double)h->hop);
+    }
+    h->q = qd;
+    h->p_mod = pn % qd;
+    h->q_pow2 = is_pow2((long long)qd) ? 1 : 0;
+    h->inv_q = (float)(1.0 / (double)qd);
+    if (!h->q_pow2 && qd > 32768) return bail(fail(PV_ERR_UNSUPPORTED, "output-phase ratio denominator too large"));
+    std::vector<unsigned> jkm(B);
+    for (int k = 0; k < B; ++k) {
+        unsigned long long v = ((pn % qd) * ((unsigned long long)jk[k] % qd)) % qd;
+        jkm[k] = (unsigned)v;
+    }
+    if ((st = upload(&h->d_ek, ek)) != PV_OK) return bail(st);
+    if ((st = upload(&h->d_jk_mod, jkm)) != PV_OK) return bail(st);
+
+    // ---- pitch map: k' = floor(beta*k + 0.5) (magnitudes summed, phase from smallest k)
+    std::vector<int> first(B, -1), cnt(B, 0);
+    if (h->pitch) {
+        const double beta = (double)cfg->scale;
+        for (int k = 0; k < B; ++k) {
+            long long kp = (long long)std::floor(beta * (double)k + 0.5);
+            if (kp < 0 || kp >= B) continue;
+            if (first[kp] < 0) first[kp] = k;
+            cnt[kp]++;
+        }
+    }
+    if ((st = upload(&h->d_src_first, first)) != PV_OK) return bail(st);
+    if ((st = upload(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
+
+    // ---- workspace
+    const size_t runs_total = (size_t)std::max(cfg->max_channels, 1) * std::max(h->max_runs, 1);
+    if (h->mode == PV_MODE_STANDARD) {
+        PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * h->bins_pad));
+        PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
+    }
+    PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * runs_total * h->tail_len));
+
+    // LDS budget check for the synthesis kernel (largest)
+    size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->bins_pad, h->ring);
+    if (lds > 160 * 1024) return bail(fail(PV_ERR_UNSUPPORTED, "LDS budget exceeded"));
+    *out = h;
+    return PV_OK;
+}
+
+pv_status pv_analysis(pv_handle* h, const float* x, long long ldx, long long n_samples,
+                      int channels, int frames, pv_float2* spec, long long ld_spec, void* stream) {
+    pv_status st = check_common(h, channels, frames);
+    if (st != PV_OK) return st;
+    DeviceGuard g(h->cfg.device);
+    return do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, false,
+                       (hipStream_t)stream);
+}
+
+pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                         int frames, const float* ola_in, long long ld_ola, float* out,
+                         long long ldo, void* stream) {
+    pv_status st = check_common(h, channels, frames);
+    if (st != PV_OK) return st;
+    DeviceGuard g(h->cfg.device);
+    return do_resynthesis(h, spec, ld_spec, channels, frames, ola_in, ld_ola, out, ldo, false,
+                          (hipStream_t)stream);
+}
+
+pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
+                     int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
+                     long long ldo, void* stream) {
+    pv_status st = check_common(h, channels, frames);
+    if (st != PV_OK) return st;
+    DeviceGuard g(h->cfg.device);
+    hipStream_t s = (hipStream_t)stream;
+    const bool std_mode = (h->mode == PV_MODE_STANDARD);
+    st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
+    if (st != PV_OK) return st;
+    return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
+}
+
+pv_status pv_profile_enable(pv_handle* h, int enable) {
+    if (!h) return fail(PV_ERR_ARG, "null handle");
+    h->prof.enabled = enable != 0;
+    return PV_OK;
+}
+
+int pv_profile_read(pv_handle* h, const char** names, double* total_ms, int* launches, int cap) {
+    if (!h) return 0;
+    DeviceGuard g(h->cfg.device);
+    for (size_t i = 0; i < h->prof.ev_start.size(); ++i) {
+        float ms = 0.f;
+        if (hipEventSynchronize(h->prof.ev_stop[i]) == hipSuccess &&
+            hipEventElapsedTime(&ms, h->prof.ev_start[i], h->prof.ev_stop[i]) == hipSuccess) {
+            h->prof.total_ms[h->prof.ev_kernel[i]] += ms;
+            h->prof.launches[h->prof.ev_kernel[i]] += 1;
+        }
+        (void)hipEventDestroy(h->prof.ev_start[i]);
+        (void)hipEventDestroy(h->prof.ev_stop[i]);
+    }
+    h->prof.ev_start.clear();
+    h->prof.ev_stop.clear();
+    h->prof.ev_kernel.clear();
+    int n = 0;
+    for (int k = 0; k < kNumKernels && n < cap; ++k) {
+        if (h->prof.launches[k] == 0) continue;
+        if (names) names[n] = kKernelNames[k];
+        if (total_ms) total_ms[n] = h->prof.total_ms[k];
+        if (launches) launches[n] = h->prof.launches[k];
+        ++n;
+    }
+    return n;
+}
+
+void pv_profile_reset(pv_handle* h) {
+    if (!h) return;
+    (void)pv_profile_read(h, nullptr, nullptr, nullptr, 0);
+    for (int k = 0; k < kNumKernels; ++k) {
+        h->prof.total_ms[k] = 0;
+        h->prof.launches[k] = 0;
+    }
+}
+
+}  // extern "C"

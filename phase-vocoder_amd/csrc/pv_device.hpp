@@ -1,0 +1,182 @@
+// pv_device.hpp — CDNA4 device building blocks of the phase-vocoder hot path.
+//
+// One frame per wavefront: the L complex points of a frame's FFT live in the 64 lanes'
+// registers (E = L/64 per lane) and in one per-wave LDS tile between passes.  Each pass
+// performs log2(E) radix-2 Stockham stages entirely in registers; a pass is exactly the
+// composition of the radix-2 stages of hpfft.cu:145-167 (same butterfly, same tabled
+// twiddle per butterfly), so the result is bit-identical to the oracle's radix-2
+// restatement (oracle/pvref.c pvr_fft_c32) — only the LDS round trips are removed.
+//
+// Compiled with -ffp-contract=off: every fp32 operation below is the one written, and
+// fmaf() marks the fused operations of the numerical contract.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pv {
+
+constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
+constexpr int bitrevc(int v, int bits) {
+    int r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((v >> i) & 1) << (bits - 1 - i);
+    return r;
+}
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+
+// ------------------------------------------------------------------ fp32 contract
+constexpr float kHalfPi = 0x1.921fb6p+0f;
+constexpr float kPi = 0x1.921fb6p+1f;
+constexpr float kTwoPi = 0x1.921fb6p+2f;
+constexpr float kInv2Pi = 0x1.45f306p-3f;
+
+__device__ __forceinline__ float2 cmul(float2 b, float2 w) {
+    float2 t;
+    t.x = __builtin_fmaf(b.x, w.x, -(b.y * w.y));
+    t.y = __builtin_fmaf(b.x, w.y, b.y * w.x);
+    return t;
+}
+
+// atan2 of the contract (oracle pvr_atan2f); atan(a) = a*P(a^2), |err| <= 2.7e-7 rad.
+__device__ __forceinline__ float atan2_pv(float y, float x) {
+    float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+    bool xg = ax > ay;
+    float mx = xg ? ax : ay;
+    float mn = xg ? ay : ax;
+    float a = mn / mx;  // IEEE division (-fhip-fp32-correctly-rounded-divide-sqrt)
+    float s = a * a;
+    float p = -0x1.8ba68ap-10f;
+    p = __builtin_fmaf(p, s, 0x1.398008p-7f);
+    p = __builtin_fmaf(p, s, -0x1.d2ca58p-6f);
+    p = __builtin_fmaf(p, s, 0x1.c2c9f4p-5f);
+    p = __builtin_fmaf(p, s, -0x1.506f6cp-4f);
+    p = __builtin_fmaf(p, s, 0x1.bd9028p-4f);
+    p = __builtin_fmaf(p, s, -0x1.23c87ap-3f);
+    p = __builtin_fmaf(p, s, 0x1.9986ecp-3f);
+    p = __builtin_fmaf(p, s, -0x1.5554eep-2f);
+    p = __builtin_fmaf(p, s, 0x1.000000p+0f);
+    float r = a * p;
+    if (ay > ax) r = kHalfPi - r;
+    if (x < 0.0f) r = kPi - r;
+    if (y < 0.0f) r = -r;
+    return (mx == 0.0f) ? 0.0f : r;  // phase of an exactly-zero bin := +0
+}
+
+// unwrap decision of the contract (oracle pvr_unwrap_count)
+__device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) {
+    float d = (phi - phi_prev) - e;
+    float q = d * kInv2Pi;
+    return -(int)__builtin_rintf(q);
+}
+
+// ------------------------------------------------------------------ wave-local LDS sync
+// A frame's LDS tile is private to one wave; LDS executes a wave's DS instructions in
+// order, so a compiler fence + wave barrier orders the cross-lane exchange.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------------ FFT geometry
+template <int L_>
+struct Geo {
+    static constexpr int L = L_;
+    static constexpr int LOG2L = ilog2c(L);
+    static constexpr int E = L / 64;                 // complex points per lane
+    static constexpr int RLOG = ilog2c(E);           // stages per full pass
+    static constexpr int NPASS = (LOG2L + RLOG - 1) / RLOG;
+    static constexpr int PADSH = RLOG;               // one pad slot every E points
+    static constexpr int TILE = L + (L >> PADSH) + 2;  // padded LDS tile (float2), +bin L
+    static_assert(L >= 128 && L <= 2048, "one frame per wave: L in [128, 2048]");
+    __device__ static __forceinline__ int pad(int p) { return p + (p >> PADSH); }
+};
+
+// Stage-major twiddle table: stage Ns occupies [Ns-1, 2Ns-1), entry idx = e^{-i pi idx/Ns}
+// (the values of the oracle's master table tw[idx*L/(2Ns)], copied, so bit-identical).
+
+// One register pass: P-th pass, INV selects conjugated twiddles.
+// Input layout : v[g*R + q] = x[j + q*L/R],   j = lane + 64 g
+// Output layout: v[g*R + f] = y[(j/S)*R*S + j%S + S*bitrev_r(f)]
+template <int L, int P, bool INV>
+__device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* tw, int lane) {
+    using G_ = Geo<L>;
+    constexpr int S = 1 << (P * G_::RLOG);
+    constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
+    constexpr int R = 1 << r;
+    constexpr int NG = G_::E / R;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int j = lane + 64 * g;
+        const int jm = j & (S - 1);
+        float2 a[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) a[q] = v[g * R + q];
+#pragma unroll
+        for (int st = 0; st < r; ++st) {
+            const int Ns = S << st;
+            float2 b[R];
+#pragma unroll
+            for (int s = 0; s < R / 2; ++s) {
+                const int br = bitrevc(s & ((1 << st) - 1), st);
+                float2 w = tw[(Ns - 1) + jm + S * br];
+                if (INV) w.y = -w.y;
+                const float2 top = a[s];
+                const float2 t = cmul(a[s + R / 2], w);
+                b[2 * s].x = top.x + t.x;
+                b[2 * s].y = top.y + t.y;
+                b[2 * s + 1].x = top.x - t.x;
+                b[2 * s + 1].y = top.y - t.y;
+            }
+#pragma unroll
+            for (int q = 0; q < R; ++q) a[q] = b[q];
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[g * R + q] = a[q];
+    }
+}
+
+template <int L, int P>
+__device__ __forceinline__ void pass_store(const float2 (&v)[Geo<L>::E], float2* tile, int lane) {
+    using G_ = Geo<L>;
+    constexpr int S = 1 << (P * G_::RLOG);
+    constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
+    constexpr int R = 1 << r;
+    constexpr int NG = G_::E / R;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int j = lane + 64 * g;
+        const int J = (j / S) * R * S + (j & (S - 1));
+#pragma unroll
+        for (int f = 0; f < R; ++f) tile[G_::pad(J + S * bitrevc(f, r))] = v[g * R + f];
+    }
+}
+
+template <int L, int P>
+__device__ __forceinline__ void pass_load(float2 (&v)[Geo<L>::E], const float2* tile, int lane) {
+    using G_ = Geo<L>;
+    constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
+    constexpr int R = 1 << r;
+    constexpr int NG = G_::E / R;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int j = lane + 64 * g;
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[g * R + q] = tile[G_::pad(j + q * (L / R))];
+    }
+}
+
+// Full FFT: v holds the pass-0 input layout (x[lane + 64 q], since R0 = E); the result is
+// left in `tile` in natural order (padded indexing).
+template <int L, bool INV, int P = 0>
+__device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, const float2* tw,
+                                        int lane) {
+    fft_pass<L, P, INV>(v, tw, lane);
+    pass_store<L, P>(v, tile, lane);
+    wave_lds_sync();
+    if constexpr (P + 1 < Geo<L>::NPASS) {
+        pass_load<L, P + 1>(v, tile, lane);
+        wave_lds_sync();
+        fft_run<L, INV, P + 1>(v, tile, tw, lane);
+    }
+}
+
+}  // namespace pv

@@ -1,0 +1,77 @@
+// pv_kernels.h — kernel parameter blocks and launchers (host <-> device interface of libpv).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace pv {
+
+struct AnaParams {
+    const float* x;
+    long long ldx, n;
+    int hop, frames, F, nruns;
+    int aligned;            // x base, ldx and hop allow 8-byte vector loads
+    const float* win;       // analysis window (N)
+    const float2* tw;       // stage-major twiddles of the L-point FFT (L entries)
+    const float2* tws;      // real-split twiddles e^{-2 pi i k / (2L)}, k <= L
+    const float* ek;        // expected advance (STANDARD), bins
+    float2* spec;
+    long long ld_spec;
+    int spec_stride;
+    int* runsum;            // [C][nruns][bins_pad] or nullptr
+    int bins_pad;
+    int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
+};
+
+struct ScanParams {
+    const float2* spec;
+    long long ld_spec;
+    int spec_stride, frames, F, nruns, L, bins_pad;
+    const float* ek;
+    int* runsum;
+    int* carry;
+};
+
+struct SynParams {
+    const float2* spec;
+    long long ld_spec;
+    int spec_stride, frames, F, nruns, bins_pad;
+    const int* carry;
+    const float* ek;
+    const unsigned* jk_mod;            // (p * j_k) mod q
+    const int* src_first;              // pitch map
+    const int* src_cnt;
+    int pitch;
+    float rho;
+    unsigned long long p_mod, q;
+    int q_pow2;
+    float inv_q;
+    const float2* tw;                  // stage-major twiddles, L-point
+    const float2* tws;                 // e^{-2 pi i k/N}, k <= L
+    const float* gain;                 // synthesis window * norm / N   (N)
+    int rot;                           // 0 (STANDARD) or N/2 (REF_COMPAT swap halves)
+    int hs;                            // out hop
+    int ring_size;                     // power of 2 >= 4*hs + N
+    float* out;
+    long long ldo, out_len;
+    float* tails;                      // [C][nruns][tail_len]
+    int tail_len;
+};
+
+struct SeamParams {
+    float* out;
+    long long ldo, out_len;
+    const float* tails;
+    const float* ola_in;
+    long long ld_ola;
+    int nruns, F, hs, tail_len;
+};
+
+hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
+hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
+hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
+hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
+hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
+hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
+size_t synthesis_lds_bytes(int L, int bins_pad, int ring);
+
+}  // namespace pv

@@ -1,0 +1,8 @@
+"""pvamd — host-side mirror of the reference's PhaseVocoder interface over libpv.so
+(the MI355X HIP phase-vocoder hot path).  See DESIGN.md and include/pv.h."""
+from ._lib import PVError, frame_count, lib  # noqa: F401
+from .vocoder import (PITCH_SHIFT, REF_COMPAT, STANDARD, TIME_SHIFT,  # noqa: F401
+                      PhaseVocoder)
+
+__all__ = ["PhaseVocoder", "PVError", "TIME_SHIFT", "PITCH_SHIFT", "REF_COMPAT", "STANDARD",
+           "frame_count", "lib"]

@@ -1,0 +1,95 @@
+"""ctypes binding of libpv.so (include/pv.h).  Loads the in-tree build and fails loudly
+if it is missing: there is no CPU fallback in the product path."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(_PKG, "..", ".."))
+LIB_PATH = os.path.join(_PKG, "..", "build", "libpv.so")
+HEADER = os.path.join(ROOT, "include", "pv.h")
+
+PV_OK, PV_ERR_ARG, PV_ERR_UNSUPPORTED, PV_ERR_HIP, PV_ERR_NOMEM = range(5)
+PV_TIME_SHIFT, PV_PITCH_SHIFT = ord("t"), ord("p")
+PV_MODE_REF_COMPAT, PV_MODE_STANDARD = 0, 1
+
+
+class PVError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{msg} (status {status})")
+        self.status = status
+
+
+class pv_config(ctypes.Structure):
+    _fields_ = [("n_samps", ctypes.c_int), ("hop_div", ctypes.c_int), ("effect", ctypes.c_int),
+                ("scale", ctypes.c_float), ("mode", ctypes.c_int), ("max_channels", ctypes.c_int),
+                ("max_frames", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+class pv_info(ctypes.Structure):
+    _fields_ = [("n_samps", ctypes.c_int), ("hop", ctypes.c_int), ("out_hop", ctypes.c_int),
+                ("spec_bins", ctypes.c_int), ("spec_stride", ctypes.c_int),
+                ("frames_per_run", ctypes.c_int), ("mode", ctypes.c_int), ("effect", ctypes.c_int),
+                ("scale", ctypes.c_float)]
+
+
+_lib = None
+
+
+def declared_symbols() -> list[str]:
+    """Function names declared in include/pv.h (the ABI contract)."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(pv_\w+)\s*\(", txt, flags=re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PVError(-1, f"libpv.so not built at {LIB_PATH}: run `make -C phase-vocoder_amd/csrc` "
+                          "(no CPU fallback exists)")
+    L = ctypes.CDLL(os.path.abspath(LIB_PATH))
+    vp, ll, i, f = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
+    L.pv_abi_version.restype = i
+    L.pv_status_string.argtypes = [i]
+    L.pv_status_string.restype = ctypes.c_char_p
+    L.pv_last_error.restype = ctypes.c_char_p
+    L.pv_create.argtypes = [ctypes.POINTER(pv_config), ctypes.POINTER(vp)]
+    L.pv_create.restype = i
+    L.pv_destroy.argtypes = [vp]
+    L.pv_destroy.restype = None
+    L.pv_get_info.argtypes = [vp, ctypes.POINTER(pv_info)]
+    L.pv_get_info.restype = i
+    L.pv_frame_count.argtypes = [ll, i]
+    L.pv_frame_count.restype = i
+    L.pv_output_length.argtypes = [vp, i]
+    L.pv_output_length.restype = ll
+    L.pv_analysis.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp]
+    L.pv_analysis.restype = i
+    L.pv_resynthesis.argtypes = [vp, vp, ll, i, i, vp, ll, vp, ll, vp]
+    L.pv_resynthesis.restype = i
+    L.pv_process.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, vp]
+    L.pv_process.restype = i
+    L.pv_profile_enable.argtypes = [vp, i]
+    L.pv_profile_enable.restype = i
+    L.pv_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_int), i]
+    L.pv_profile_read.restype = i
+    L.pv_profile_reset.argtypes = [vp]
+    L.pv_profile_reset.restype = None
+    _lib = L
+    return L
+
+
+def check(status: int, what: str = "pv call"):
+    if status != PV_OK:
+        L = lib()
+        raise PVError(status, f"{what}: {L.pv_status_string(status).decode()}: "
+                              f"{L.pv_last_error().decode()}")
+
+
+def frame_count(n_samples: int, hop: int) -> int:
+    return lib().pv_frame_count(int(n_samples), int(hop))

@@ -1,0 +1,205 @@
+"""Python mirror of the reference's `PhaseVocoder` / `CudaPhase` surface over libpv.
+
+Same names, argument meaning and (optionally) the print-and-exit error behaviour of the
+reference, so parity tests read like src/main.cpp:
+  PhaseVocoder(samples, effect, scaleFactor, hop)      src/phaseVocoder.h:79-116
+  .nSamps .hopSize .outHopSize .timeScale .imp          src/phaseVocoder.h:16-31
+  .analysis_CUFFT(input, output, fft, intermediary)     src/phaseVocoder.cpp:25-33
+  .resynthesis_CUFFT(backFrame, frontFrame, output)     src/phaseVocoder.cpp:60-76
+plus the batched entry points the MI355X design is built around (analysis / resynthesis /
+process over channels x frames).  Tensors are torch CUDA tensors (device memory and the
+current stream are the only things torch provides here).
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+
+import numpy as np
+
+from . import _lib
+from ._lib import PV_MODE_REF_COMPAT, PV_MODE_STANDARD, PVError
+
+TIME_SHIFT = "t"  # phaseVocoder.h:6
+PITCH_SHIFT = "p"  # phaseVocoder.h:7
+REF_COMPAT = "ref_compat"
+STANDARD = "standard"
+
+
+def _torch():
+    import torch  # plumbing only: device memory + streams
+
+    return torch
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+class PhaseVocoder:
+    """`class PhaseVocoder` (src/phaseVocoder.h:9-139) on the MI355X HIP path."""
+
+    def __init__(self, samples: int, effect: str = TIME_SHIFT, scaleFactor: float = 1.0,
+                 hop: int = 2, *, mode: str = REF_COMPAT, max_channels: int = 1,
+                 max_frames: int = 4096, device: int = 0, exit_on_error: bool = False):
+        self.exit_on_error = exit_on_error
+        eff = effect if isinstance(effect, int) else ord(effect)
+        m = PV_MODE_REF_COMPAT if mode == REF_COMPAT else PV_MODE_STANDARD
+        cfg = _lib.pv_config(int(samples), int(hop), eff, float(scaleFactor), m,
+                             int(max_channels), int(max_frames), int(device))
+        h = ctypes.c_void_p()
+        self._L = _lib.lib()
+        self._call(self._L.pv_create(ctypes.byref(cfg), ctypes.byref(h)), "pv_create")
+        self._h = h
+        info = _lib.pv_info()
+        self._call(self._L.pv_get_info(self._h, ctypes.byref(info)), "pv_get_info")
+        self.info = info
+        self.device = int(device)
+        self.mode = mode
+        self.effect = chr(eff)
+        # field names of phaseVocoder.h
+        self.nSamps = info.n_samps
+        self.N = info.n_samps
+        self.hopSize = info.hop
+        self.outHopSize = info.out_hop
+        self.timeScale = float(scaleFactor) if self.effect == TIME_SHIFT else 1.0
+        self.spec_bins = info.spec_bins
+        self.spec_stride = info.spec_stride
+        self.frames_per_run = info.frames_per_run
+
+    # -------------------------------------------------------------- plumbing
+    def _call(self, status, what):
+        if status != _lib.PV_OK:
+            if self.exit_on_error:  # the reference's checkCUDAError_ (io.cpp:115-124)
+                L = _lib.lib()
+                print(f"Cuda error: {what}: {L.pv_last_error().decode()}.", file=sys.stderr)
+                sys.exit(1)
+            _lib.check(status, what)
+
+    def _stream(self, stream=None):
+        if stream is not None:
+            return ctypes.c_void_p(int(stream))
+        torch = _torch()
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.pv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def imp(self) -> np.ndarray:
+        """Analysis window (phaseVocoder.h:16 `imp`), host copy."""
+        from .tables import analysis_window
+        return analysis_window(self.nSamps, self.mode)
+
+    # -------------------------------------------------------------- geometry
+    def num_frames(self, n_samples: int) -> int:
+        return _lib.frame_count(n_samples, self.hopSize)
+
+    def output_length(self, frames: int) -> int:
+        return int(self._L.pv_output_length(self._h, int(frames)))
+
+    def alloc_spec(self, channels: int, frames: int):
+        torch = _torch()
+        return torch.zeros((channels, frames, self.spec_stride, 2), dtype=torch.float32,
+                           device=f"cuda:{self.device}")
+
+    def alloc_out(self, channels: int, frames: int):
+        torch = _torch()
+        return torch.empty((channels, self.output_length(frames)), dtype=torch.float32,
+                           device=f"cuda:{self.device}")
+
+    # -------------------------------------------------------------- batched API
+    @staticmethod
+    def _as2d(x):
+        return x.unsqueeze(0) if x.dim() == 1 else x
+
+    def analysis(self, x, frames: int | None = None, n_samples: int | None = None, spec=None,
+                 stream=None):
+        """x: [C, n] (or [n]) float32 CUDA -> spec [C, frames, spec_stride, 2]."""
+        x = self._as2d(x)
+        assert x.is_cuda and x.dtype.is_floating_point and x.stride(-1) == 1
+        C, n = x.shape
+        n_samples = n if n_samples is None else n_samples
+        frames = self.num_frames(n_samples) if frames is None else frames
+        if spec is None:
+            spec = self.alloc_spec(C, frames)
+        self._call(self._L.pv_analysis(self._h, _ptr(x), x.stride(0), n_samples, C, frames,
+                                       _ptr(spec), spec.stride(0) // 2, self._stream(stream)),
+                   "pv_analysis")
+        return spec
+
+    def resynthesis(self, spec, frames: int | None = None, out=None, ola_in=None, stream=None):
+        """spec [C, frames, spec_stride, 2] -> out [C, frames*outHop + N - outHop]."""
+        C = spec.shape[0]
+        frames = spec.shape[1] if frames is None else frames
+        if out is None:
+            out = self.alloc_out(C, frames)
+        ld_ola = 0 if ola_in is None else self._as2d(ola_in).stride(0)
+        self._call(self._L.pv_resynthesis(self._h, _ptr(spec), spec.stride(0) // 2, C, frames,
+                                          _ptr(ola_in), ld_ola, _ptr(out), out.stride(0),
+                                          self._stream(stream)), "pv_resynthesis")
+        return out
+
+    def process(self, x, frames: int | None = None, n_samples: int | None = None, spec=None,
+                out=None, stream=None):
+        """analysis -> processing -> resynthesis; returns (out, spec)."""
+        x = self._as2d(x)
+        C, n = x.shape
+        n_samples = n if n_samples is None else n_samples
+        frames = self.num_frames(n_samples) if frames is None else frames
+        if spec is None:
+            spec = self.alloc_spec(C, frames)
+        if out is None:
+            out = self.alloc_out(C, frames)
+        self._call(self._L.pv_process(self._h, _ptr(x), x.stride(0), n_samples, C, frames,
+                                      _ptr(spec), spec.stride(0) // 2, _ptr(out), out.stride(0),
+                                      self._stream(stream)), "pv_process")
+        return out, spec
+
+    # -------------------------------------------------------------- reference per-frame API
+    def analysis_CUFFT(self, input, output, fft=None, intermediary=None):
+        """PhaseVocoder::analysis_CUFFT (phaseVocoder.cpp:25-33): one frame of nSamps
+        samples starting at `input` -> `output` (2N float2 in REF_COMPAT).  `fft` and
+        `intermediary` are accepted for signature parity and unused (as in the reference
+        the cuFFT path never touches `fft`; the window product stays on chip here)."""
+        self._call(self._L.pv_analysis(self._h, _ptr(input), self.nSamps, self.nSamps, 1, 1,
+                                       _ptr(output), self.spec_stride, self._stream()),
+                   "analysis_CUFFT")
+
+    def resynthesis_CUFFT(self, backFrame, frontFrame, output):
+        """PhaseVocoder::resynthesis_CUFFT (phaseVocoder.cpp:60-76): output[0..N) =
+        frame(frontFrame) + backFrame[outHop..N) shifted to the front (cudaOverlapAdd,
+        kernel.cu:111-119)."""
+        ola = backFrame[self.outHopSize:]
+        self._call(self._L.pv_resynthesis(self._h, _ptr(frontFrame), self.spec_stride, 1, 1,
+                                          _ptr(ola), self.nSamps, _ptr(output), self.nSamps,
+                                          self._stream()), "resynthesis_CUFFT")
+
+    # -------------------------------------------------------------- profiling (bench.py)
+    def profile(self, enable: bool = True):
+        self._call(self._L.pv_profile_enable(self._h, 1 if enable else 0), "pv_profile_enable")
+
+    def profile_read(self) -> dict:
+        cap = 8
+        names = (ctypes.c_char_p * cap)()
+        ms = (ctypes.c_double * cap)()
+        cnt = (ctypes.c_int * cap)()
+        n = self._L.pv_profile_read(self._h, names, ms, cnt, cap)
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
+
+    def profile_reset(self):
+        self._L.pv_profile_reset(self._h)

@@ -1,0 +1,106 @@
+"""GPU parity of the HIP path (through the C-ABI) against the CPU oracle."""
+import numpy as np
+import pytest
+
+import pvref
+from pvamd import PhaseVocoder, REF_COMPAT, STANDARD, TIME_SHIFT, PITCH_SHIFT
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-5  # BASELINE.json north_star: <= 1e-5 RMS per sample vs the CPU reference
+
+
+def synth(n, seed, sr=44100, tones=3):
+    """configs 2-4 generator: 3 sines f~U[55,4000] Hz, a=0.1, + U(+-1e-3) noise."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sr
+    x = np.zeros(n)
+    for _ in range(tones):
+        f = rng.uniform(55, 4000)
+        ph = rng.uniform(0, 2 * np.pi)
+        x += 0.1 * np.sin(2 * np.pi * f * t + ph)
+    x += rng.uniform(-1e-3, 1e-3, n)
+    return x.astype(np.float32)
+
+
+def to_dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("N,hop_div", [(1024, 4), (2048, 4), (512, 4), (256, 4), (1024, 2), (2048, 8)])
+def test_std_analysis_bit_exact(cuda, N, hop_div):
+    x = synth(20 * N, 7)
+    pv = PhaseVocoder(N, TIME_SHIFT, 1.0, hop_div, mode=STANDARD, max_frames=1000)
+    spec = pv.analysis(to_dev(x)).cpu().numpy()[0]
+    frames = pv.num_frames(len(x))
+    mag, ph = pvref.std_analysis(x, N, N // hop_div, frames)
+    g_mag, g_ph = spec[:frames, :N // 2 + 1, 0], spec[:frames, :N // 2 + 1, 1]
+    assert np.array_equal(g_ph.view(np.uint32), ph.view(np.uint32)), \
+        f"phase mismatch: {np.sum(g_ph != ph)} bins, max {np.abs(g_ph - ph).max()}"
+    assert np.array_equal(g_mag.view(np.uint32), mag.view(np.uint32)), \
+        f"mag mismatch: {np.sum(g_mag != mag)} bins, max rel {np.max(np.abs(g_mag - mag) / (mag + 1e-30))}"
+
+
+@pytest.mark.parametrize("effect,scale", [(TIME_SHIFT, 0.5), (TIME_SHIFT, 1.0), (PITCH_SHIFT, 2.0),
+                                          (PITCH_SHIFT, 1.5), (PITCH_SHIFT, 0.75), (TIME_SHIFT, 1.5)])
+def test_std_process_parity(cuda, effect, scale):
+    N, hop_div = 1024, 4
+    x = synth(3 * 44100 // 2, 20240)
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_frames=1000)
+    out, _ = pv.process(to_dev(x))
+    g = out.cpu().numpy()[0]
+    ref = pvref.std_process(x, N, hop_div, ord(effect), scale)
+    assert g.shape == ref.shape
+    err = rms(g, ref)
+    assert err <= RMS_TOL, f"rms {err}"
+
+
+def test_std_process_multichannel(cuda):
+    N, hop_div, C = 1024, 4, 5
+    xs = np.stack([synth(30000, 20240 + c) for c in range(C)])
+    pv = PhaseVocoder(N, TIME_SHIFT, 0.5, hop_div, mode=STANDARD, max_channels=C, max_frames=200)
+    out, _ = pv.process(to_dev(xs))
+    g = out.cpu().numpy()
+    ref, _ = pvref.std_process_batch(xs, N, hop_div, ord("t"), 0.5)
+    for c in range(C):
+        assert rms(g[c], ref[c]) <= RMS_TOL
+
+
+def test_split_equals_fused(cuda):
+    N, hop_div = 1024, 4
+    x = synth(40000, 3)
+    pv = PhaseVocoder(N, PITCH_SHIFT, 1.5, hop_div, mode=STANDARD, max_frames=400)
+    out1, spec1 = pv.process(to_dev(x))
+    spec2 = pv.analysis(to_dev(x))
+    out2 = pv.resynthesis(spec2)
+    assert np.array_equal(spec1.cpu().numpy(), spec2.cpu().numpy())
+    assert np.array_equal(out1.cpu().numpy(), out2.cpu().numpy())
+
+
+@pytest.mark.parametrize("N,hop_div", [(1024, 4), (256, 2), (512, 4), (2048, 4)])
+def test_ref_compat_parity(cuda, N, hop_div):
+    x = synth(30000, 11)
+    pv = PhaseVocoder(N, TIME_SHIFT, 1.0, hop_div, mode=REF_COMPAT, max_frames=1000)
+    out, spec = pv.process(to_dev(x))
+    g = out.cpu().numpy()[0]
+    ref = pvref.compat_process(x, N, hop_div)
+    assert g.shape == ref.shape
+    err = rms(g, ref)
+    assert err <= RMS_TOL, f"rms {err}"
+
+
+def test_ref_compat_spectrum(cuda):
+    N = 1024
+    x = synth(N, 5)
+    pv = PhaseVocoder(N, TIME_SHIFT, 1.0, 4, mode=REF_COMPAT, max_frames=4)
+    spec = pv.analysis(to_dev(x), frames=1, n_samples=N).cpu().numpy()[0, 0]
+    ref = pvref.compat_analysis_frame(x, N)
+    mag_ref = ref.real
+    assert np.max(np.abs(spec[:2 * N, 0] - mag_ref)) <= 1e-5 * np.max(mag_ref)
+    big = mag_ref > 1e-3 * mag_ref.max()
+    assert np.max(np.abs(spec[:2 * N, 1][big] - ref.imag[big])) < 1e-3
