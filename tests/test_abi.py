@@ -1,0 +1,73 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/pv.h declares,
+and its host-only helpers behave (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from pvamd import _lib
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    L = _lib.lib()
+    declared = _lib.declared_symbols()
+    assert len(declared) >= 14
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in nm.splitlines() if " T " in ln}
+    assert set(declared) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_abi_version_and_status_strings():
+    L = _lib.lib()
+    assert L.pv_abi_version() == 1
+    assert L.pv_status_string(0) == b"PV_OK"
+    assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
+
+
+def test_frame_count_is_main_cpp_loop():
+    # main.cpp:231  for (i = 0; i < numSamples - hopSize; i += hopSize)
+    def loop(n, hop):
+        c, i = 0, 0
+        while i < n - hop:
+            c += 1
+            i += hop
+        return c
+    for n in (0, 1, 255, 256, 257, 1000, 441000, 2646000):
+        for hop in (64, 128, 256, 512):
+            assert _lib.frame_count(n, hop) == loop(n, hop)
+
+
+def test_create_rejects_bad_configs_without_touching_gpu():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    for cfg in (_lib.pv_config(1000, 4, ord("t"), 1.0, 1, 1, 10, 0),   # N not a power of 2
+                _lib.pv_config(1024, 0, ord("t"), 1.0, 1, 1, 10, 0),   # hop_div 0
+                _lib.pv_config(1024, 4, ord("x"), 1.0, 1, 1, 10, 0),   # bad effect
+                _lib.pv_config(1024, 4, ord("t"), -1.0, 1, 1, 10, 0),  # bad scale
+                _lib.pv_config(1024, 4, ord("p"), 2.0, 0, 1, 10, 0)):  # compat has no pitch
+        st = L.pv_create(ctypes.byref(cfg), ctypes.byref(h))
+        assert st in (_lib.PV_ERR_ARG, _lib.PV_ERR_UNSUPPORTED)
+        assert len(L.pv_last_error()) > 0
+
+
+def test_product_does_not_reference_oracle():
+    root = _lib.ROOT
+    for dirpath, _, files in os.walk(os.path.join(root, "phase-vocoder_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                code = [ln for ln in open(os.path.join(dirpath, f)).read().splitlines()
+                        if not ln.lstrip().startswith(("//", "#", "*", "/*")) or ln.lstrip().startswith("#include")]
+                txt = "\n".join(code)
+                for bad in ("import pvref", "from pvref", "libpvref", "oracle/", "pvr_"):
+                    assert bad not in txt, (f, bad)

@@ -1,0 +1,246 @@
+"""CPU tests pinning the oracle (oracle/pvref.c) to the DFT contract, to golden vectors
+produced from the reference's own fixtures by an independent numpy restatement
+(tests/golden/make_golden.py), and to the reference's output artifact signature."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pvref
+from conftest import GOLDEN
+
+
+def g(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+# ------------------------------------------------------------ FFT contract
+@pytest.mark.parametrize("L", [2, 4, 8, 16, 64, 128, 256, 512, 1024, 2048, 4096])
+def test_fft_c32_matches_dft(L):
+    rng = np.random.default_rng(L)
+    z = (rng.standard_normal(L) + 1j * rng.standard_normal(L)).astype(np.complex64)
+    ref = np.fft.fft(z.astype(np.complex128))
+    got = pvref.fft_c32(z)
+    assert np.max(np.abs(got - ref)) <= 2e-7 * np.log2(max(L, 2)) * np.sqrt(L) * np.max(np.abs(z)) * 4
+    inv = pvref.fft_c32(z, inverse=True)
+    assert np.allclose(inv, np.fft.ifft(z.astype(np.complex128)) * L, atol=1e-5 * np.sqrt(L))
+
+
+def test_fft_known_answers():
+    L = 256
+    imp = np.zeros(L, np.complex64)
+    imp[0] = 1
+    assert np.array_equal(pvref.fft_c32(imp), np.ones(L, np.complex64))  # impulse -> flat
+    dc = np.ones(L, np.complex64)
+    out = pvref.fft_c32(dc)
+    assert out[0] == L and np.max(np.abs(out[1:])) < 1e-4  # DC -> single bin
+    k0 = 7
+    cos = np.cos(2 * np.pi * k0 * np.arange(L) / L).astype(np.complex64)
+    out = pvref.fft_c32(cos)
+    assert abs(out[k0] - L / 2) < 1e-3 and abs(out[L - k0] - L / 2) < 1e-3
+    mask = np.ones(L, bool)
+    mask[[k0, L - k0]] = False
+    assert np.max(np.abs(out[mask])) < 1e-3
+
+
+@pytest.mark.parametrize("name", ["50Hz", "50Hz+500Hz", "500Hz+505Hz+12000Hz"])
+def test_fft_on_reference_dat_fixtures(name):
+    v = g(f"dat_{name}.npy")[:512]
+    ref = g(f"dft_{name}_512.npy")
+    got = pvref.fft_c32(v.astype(np.complex64))
+    assert np.max(np.abs(got - ref)) <= 1e-6 * np.max(np.abs(ref)) * 10
+    got64 = pvref.fft_c64(v.astype(np.complex128))
+    assert np.allclose(got64, ref, atol=1e-12 * np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("N", [256, 512, 1024, 2048, 4096])
+def test_rfft_contract(N):
+    rng = np.random.default_rng(N)
+    x = rng.standard_normal(N).astype(np.float32)
+    X = pvref.rfft_c32(x)
+    ref = np.fft.rfft(x.astype(np.float64))
+    assert np.max(np.abs(X - ref)) <= 3e-7 * np.max(np.abs(ref)) * np.log2(N)
+    assert X[0].imag == 0 and X[-1].imag == 0
+
+
+def test_atan2_contract_accuracy():
+    rng = np.random.default_rng(3)
+    ys = rng.standard_normal(20000).astype(np.float32)
+    xs = rng.standard_normal(20000).astype(np.float32)
+    got = np.array([pvref.atan2f(a, b) for a, b in zip(ys, xs)], np.float64)
+    err = np.max(np.abs(got - np.arctan2(ys.astype(np.float64), xs.astype(np.float64))))
+    assert err <= 3e-7
+    assert pvref.atan2f(0.0, 0.0) == 0.0 and pvref.atan2f(-0.0, -0.0) == 0.0  # zero bin := 0
+    assert pvref.atan2f(1.0, 0.0) == np.float32(np.pi / 2)
+    assert pvref.atan2f(-1.0, 0.0) == -np.float32(np.pi / 2)
+    assert pvref.atan2f(0.0, -1.0) == np.float32(np.pi)
+
+
+def test_unwrap_count():
+    e = np.float32(0.0)
+    assert pvref.unwrap_count(3.0, -3.0, e) == -1      # +6 rad -> wrap down
+    assert pvref.unwrap_count(-3.0, 3.0, e) == 1
+    assert pvref.unwrap_count(0.5, 0.1, e) == 0
+    # decisions on exact half-turns round to even
+    assert pvref.unwrap_count(np.float32(np.pi), 0.0, e) in (0, -1)
+
+
+def test_expected_advance_tables():
+    N, hop = 1024, 256
+    e, j = pvref.expected_advance(N, hop)
+    k = np.arange(N // 2 + 1)
+    full = 2 * np.pi * k * hop / N
+    assert np.allclose(e + 2 * np.pi * j, full, atol=1e-5)
+    assert np.all(e <= np.float32(np.pi)) and np.all(e > -np.pi)
+
+
+def test_hamming_window_recipe():
+    # phaseVocoder.h:85-89 symmetric Hamming with a float omega
+    w = pvref.hamming_ref(1024)
+    n = np.arange(1024)
+    assert np.allclose(w, 0.54 - 0.46 * np.cos(2 * np.pi * n / 1023), atol=2e-6)
+    h = pvref.hann_periodic(1024)
+    assert np.allclose(h, 0.5 - 0.5 * np.cos(2 * np.pi * n / 1024), atol=1e-7)
+
+
+def test_frame_counts_main_cpp():
+    # main.cpp:231 loop: 440sine.wav ch0, n = 441000
+    assert pvref.num_frames(441000, 256) == 1722
+    assert pvref.num_frames(441000, 128) == 3445
+    assert pvref.num_frames(2646000, 256) == 10335
+    assert pvref.num_frames(256, 256) == 0 and pvref.num_frames(0, 64) == 0
+    assert pvref.out_hop(1024, 4, pvref.TIME_SHIFT, 0.5) == 128
+    assert pvref.out_hop(1024, 4, pvref.PITCH_SHIFT, 2.0) == 256
+
+
+# ------------------------------------------------------------ REF_COMPAT vs golden
+@pytest.mark.parametrize("N,hd", [(1024, 4), (256, 2)])
+def test_compat_oracle_vs_golden_440sine(N, hd):
+    x = g("sine440_ch0_32768.npy")
+    ref = g(f"compat_sine440_N{N}_hd{hd}.npy").astype(np.float64)
+    got = pvref.compat_process(x, N, hd)
+    assert got.shape == ref.shape
+    rms = np.sqrt(np.mean((got - ref) ** 2))
+    assert rms <= 1e-7, rms  # fp64 vs fp64 (golden stored as fp32)
+
+
+@pytest.mark.parametrize("name", ["50Hz", "50Hz+500Hz", "500Hz+505Hz+12000Hz"])
+def test_compat_analysis_vs_golden_dat(name):
+    v = g(f"dat_{name}.npy")[:256]
+    mag, ph = g(f"compat_spec_{name}_N256.npy")
+    got = pvref.compat_analysis_frame(v, 256)
+    # golden and oracle differ only in the float rounding of cos() in the window recipe
+    assert np.allclose(got.real, mag, rtol=2e-6, atol=1e-7 * mag.max())
+    big = mag > 1e-6 * mag.max()
+    assert np.allclose(got.imag[big], ph[big], atol=1e-5)
+
+
+def test_compat_matches_reference_artifact_signature():
+    """output/1000hzout.wav (reference artifact): 1000 Hz in -> 2067 Hz out (octave-up
+    artifact of reading 2N-point bins as N-point bins)."""
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    x = g("sine1000_ch0_44100.npy")
+    y = pvref.compat_process(x, 256, 2)
+    seg = y[4096:4096 + 32768] * np.hanning(32768)
+    S = np.abs(np.fft.rfft(seg))
+    f = np.fft.rfftfreq(32768, 1 / 44100)
+    peak = f[np.argmax(S)]
+    assert abs(peak - meta["1000hzout_peaks_hz"][0]) < 3.0
+    top = f[np.argsort(S)[::-1][:40]]
+    assert np.any(np.abs(top - meta["1000hzout_peaks_hz"][1]) < 3.0)  # 1723 Hz spur
+
+
+# ------------------------------------------------------------ PV_STANDARD vs numpy textbook
+def textbook_pv(x, N, hop_div, effect, beta):
+    """Independent fp64 textbook phase vocoder (Dolson / Laroche-Dolson) with the build's
+    definitions (periodic Hann, princarg unwrap, phase accumulation from 0)."""
+    hop_a = N // hop_div
+    hop_s = int(np.float32(beta) * np.float32(hop_a)) if effect == "t" else hop_a
+    n = len(x)
+    A = max(0, -(-(n - hop_a) // hop_a))
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(N) / N)
+    g_ = w * hop_s / np.sum(w * w)
+    B = N // 2 + 1
+    wk = 2 * np.pi * np.arange(B) / N
+    prev = np.zeros(B)
+    acc = np.zeros(B)
+    out = np.zeros(A * hop_s + N - hop_s)
+    xp = np.concatenate([x.astype(np.float64), np.zeros(N)])
+    for t in range(A):
+        X = np.fft.rfft(xp[t * hop_a:t * hop_a + N] * w)
+        mag, ph = np.abs(X), np.angle(X)
+        d = ph - prev - wk * hop_a
+        d = d - 2 * np.pi * np.round(d / (2 * np.pi))
+        om = wk + d / hop_a
+        prev = ph
+        if effect == "t":
+            acc = acc + hop_s * om
+            Y = mag * np.exp(1j * acc)
+        else:
+            Y = np.zeros(B, np.complex128)
+            kp = np.floor(beta * np.arange(B) + 0.5).astype(int)
+            newacc = acc.copy()
+            for k in range(B):
+                if kp[k] < B:
+                    if Y[kp[k]] == 0:
+                        newacc[kp[k]] = acc[kp[k]] + hop_a * beta * om[k]
+                    Y[kp[k]] += mag[k]
+            acc = newacc
+            Y = np.abs(Y) * np.exp(1j * acc)
+        out[t * hop_s:t * hop_s + N] += np.fft.irfft(Y, N) * g_
+    return out
+
+
+@pytest.mark.parametrize("effect,beta", [("t", 0.5), ("t", 1.0), ("p", 2.0), ("p", 1.5)])
+def test_std_oracle_vs_numpy_textbook(effect, beta):
+    """Bin-centred tones: every bin with non-negligible magnitude has its deviation far
+    from +-pi, so the unwrap decisions are well-conditioned and fp32-contract analysis +
+    fp64 synthesis must agree with an all-fp64 textbook to ~1e-7."""
+    sr, N = 44100, 1024
+    t = np.arange(12000)
+    x = (0.1 * np.sin(2 * np.pi * 10 * t / N) + 0.1 * np.sin(2 * np.pi * 29 * t / N + 0.3)).astype(np.float32)
+    got = pvref.std_process(x, N, 4, ord(effect), beta)
+    ref = textbook_pv(x, N, 4, effect, beta)
+    assert got.shape == ref.shape
+    # frames that run past the end of x are zero-padded (truncated tones leak into bins
+    # whose deviation is ~+-pi): compare only output covered by complete frames
+    hs = pvref.out_hop(N, 4, ord(effect), beta)
+    full = (len(x) - N) // 256 + 1
+    rms = np.sqrt(np.mean((got[:full * hs] - ref[:full * hs]) ** 2))
+    assert rms <= 1e-7, rms
+
+
+@pytest.mark.parametrize("effect,beta", [("t", 0.5), ("p", 2.0), ("p", 1.5)])
+def test_std_oracle_vs_numpy_textbook_spectrum(effect, beta):
+    """Arbitrary tones: bins ~2 away from a tone have deviation ~+-pi, where an ulp of
+    analysis difference flips the unwrap branch, so fp32 vs fp64 outputs
+    differ sample-wise; the spectra must still agree."""
+    sr = 44100
+    t = np.arange(40000) / sr
+    x = (0.1 * np.sin(2 * np.pi * 440 * t) + 0.1 * np.sin(2 * np.pi * 1234.5 * t + 0.3)).astype(np.float32)
+    got = pvref.std_process(x, 1024, 4, ord(effect), beta)
+    ref = textbook_pv(x, 1024, 4, effect, beta)
+    seg = slice(2048, 2048 + 16384)
+    S1 = np.abs(np.fft.rfft(got[seg] * np.hanning(16384)))
+    S2 = np.abs(np.fft.rfft(ref[seg] * np.hanning(16384)))
+    f = np.fft.rfftfreq(16384, 1 / sr)
+    p1 = sorted(f[np.argsort(S1)[-2:]])
+    p2 = sorted(f[np.argsort(S2)[-2:]])
+    assert np.allclose(p1, p2, atol=3.0)
+    assert abs(np.sum(S1 ** 2) / np.sum(S2 ** 2) - 1) < 0.05
+
+
+def test_std_identity_reconstruction():
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-0.5, 0.5, 20000).astype(np.float32)
+    y = pvref.std_process(x, 1024, 4, pvref.TIME_SHIFT, 1.0)
+    assert np.max(np.abs(y[1024:19000] - x[1024:19000])) < 1e-6
+
+
+def test_std_batch_equals_single():
+    rng = np.random.default_rng(1)
+    xs = rng.uniform(-0.1, 0.1, (3, 5000)).astype(np.float32)
+    out, used = pvref.std_process_batch(xs, 512, 4, pvref.PITCH_SHIFT, 1.5, threads=2)
+    for c in range(3):
+        assert np.array_equal(out[c], pvref.std_process(xs[c], 512, 4, pvref.PITCH_SHIFT, 1.5).astype(np.float32))
