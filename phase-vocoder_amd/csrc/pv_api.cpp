@@ -88,7 +88,7 @@ struct Profile {
 struct pv_handle {
     pv_config cfg{};
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
-    int spec_bins = 0, spec_stride = 0, F = 16, ring = 0, tail_len = 0, max_runs = 0;
+    int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1;
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
@@ -250,14 +250,14 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.gain = h->d_gain;
     p.rot = (h->mode == PV_MODE_REF_COMPAT) ? h->N / 2 : 0;
     p.hs = h->hs;
-    p.ring_size = h->ring;
     p.out = out;
     p.ldo = ldo;
     p.out_len = olen;
     p.tails = h->d_tails;
     p.tail_len = h->tail_len;
     PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, h->mode == PV_MODE_STANDARD ? 0 : 1, C, p, s));
-    if (nruns > 1 || ola_in != nullptr) {
+    const int nwg = (nruns + 3) / 4;
+    if (nwg > 1 || ola_in != nullptr) {
         pv::SeamParams sm{};
         sm.out = out;
         sm.ldo = ldo;
@@ -266,6 +266,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
         sm.ola_in = ola_in;
         sm.ld_ola = ld_ola;
         sm.nruns = nruns;
+        sm.nwg = nwg;
         sm.F = h->F;
         sm.hs = h->hs;
         sm.tail_len = h->tail_len;
@@ -386,13 +387,10 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         return fail(PV_ERR_UNSUPPORTED, "FFT length outside [128, 2048]");
     }
     h->tail_len = N - h->hs;
-    // frames per run: multiple of 4 (one round = 4 waves), run span >= overlap tail
+    // frames per wave-run; a run's output span must cover the overlap tail
     int F = 16;
     while ((long long)F * h->hs < h->tail_len) F += 4;
     h->F = F;
-    int ring = 1;
-    while (ring < 4 * h->hs + N) ring <<= 1;
-    h->ring = ring;
     h->max_runs = (cfg->max_frames + F - 1) / F;
 
     DeviceGuard g(cfg->device);
@@ -488,15 +486,17 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if ((st = upload(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
 
     // ---- workspace
-    const size_t runs_total = (size_t)std::max(cfg->max_channels, 1) * std::max(h->max_runs, 1);
+    const size_t chans = (size_t)std::max(cfg->max_channels, 1);
+    const size_t runs_total = chans * std::max(h->max_runs, 1);
+    const size_t wg_total = chans * std::max((h->max_runs + 3) / 4, 1);
     if (h->mode == PV_MODE_STANDARD) {
-        PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * h->bins_pad));
+        PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * 2 * h->bins_pad));
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
     }
-    PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * runs_total * h->tail_len));
+    PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
 
     // LDS budget check for the synthesis kernel (largest)
-    size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->bins_pad, h->ring);
+    size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->bins_pad, 0);
     if (lds > 160 * 1024) return bail(fail(PV_ERR_UNSUPPORTED, "LDS budget exceeded"));
     *out = h;
     return PV_OK;

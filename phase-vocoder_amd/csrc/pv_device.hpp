@@ -60,6 +60,30 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     return (mx == 0.0f) ? 0.0f : r;  // phase of an exactly-zero bin := +0
 }
 
+// sin/cos for the bounded phases of the synthesis (|x| < 2^10): Cody-Waite reduction by
+// pi/2 in three parts + minimax polynomials on [-pi/4, pi/4] (cephes sinf/cosf
+// coefficients); |err| <= ~1.2e-7.  Replaces ocml sincosf, whose huge-argument path costs
+// registers the synthesis kernel needs for occupancy.  Not part of the bit-exact
+// contract (synthesis parity is tolerance based).
+__device__ __forceinline__ void sincos_pv(float x, float* sn, float* cs) {
+    const float j = __builtin_rintf(x * 0x1.45f306p-1f);  // x * 2/pi
+    float r = __builtin_fmaf(-j, 1.5703125f, x);
+    r = __builtin_fmaf(-j, 4.837512969970703125e-4f, r);
+    r = __builtin_fmaf(-j, 7.54978995489188216e-8f, r);
+    const float r2 = r * r;
+    float ps = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = __builtin_fmaf(r2, ps, -1.6666654611e-1f);
+    const float s = __builtin_fmaf(r * r2, ps, r);
+    float pc = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = __builtin_fmaf(r2, pc, 4.166664568298827e-2f);
+    const float c = __builtin_fmaf(r2 * r2, pc, __builtin_fmaf(-0.5f, r2, 1.0f));
+    const int q = ((int)j) & 3;
+    const float sv = (q & 1) ? c : s;
+    const float cv = (q & 1) ? s : c;
+    *sn = (q & 2) ? -sv : sv;
+    *cs = ((q + 1) & 2) ? -cv : cv;
+}
+
 // unwrap decision of the contract (oracle pvr_unwrap_count)
 __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) {
     float d = (phi - phi_prev) - e;

@@ -17,7 +17,7 @@ struct AnaParams {
     float2* spec;
     long long ld_spec;
     int spec_stride;
-    int* runsum;            // [C][nruns][bins_pad] or nullptr
+    int* runsum;            // [C][nruns][2][bins_pad] {S, m0} or nullptr
     int bins_pad;
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
 };
@@ -50,10 +50,9 @@ struct SynParams {
     const float* gain;                 // synthesis window * norm / N   (N)
     int rot;                           // 0 (STANDARD) or N/2 (REF_COMPAT swap halves)
     int hs;                            // out hop
-    int ring_size;                     // power of 2 >= 4*hs + N
     float* out;
     long long ldo, out_len;
-    float* tails;                      // [C][nruns][tail_len]
+    float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
     int tail_len;
 };
 
@@ -63,7 +62,7 @@ struct SeamParams {
     const float* tails;
     const float* ola_in;
     long long ld_ola;
-    int nruns, F, hs, tail_len;
+    int nruns, nwg, F, hs, tail_len;
 };
 
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s);

@@ -7,117 +7,186 @@
 //         exclusive integer scan of the decisions over runs -> unwrap count at run start
 //   K3  k_synthesis<MODE>   phase propagation -> polar->rect -> inverse real FFT ->
 //         window -> overlap-add of the run in an LDS ring -> plain stores
-//   K4  k_seam   adds each run's overlap tail into the next run's head
+//   K4  k_seam   adds each workgroup's overlap tail into the next workgroup's head
 //
-// Geometry: a workgroup = 4 waves owns a RUN of F consecutive frames of one channel;
-// in each round the 4 waves transform 4 consecutive frames (one frame per wavefront).
+// Geometry: one frame per wavefront, and each wave owns a RUN of F consecutive frames of
+// one channel which it walks in order (the unwrap state stays in registers, the
+// overlap-add in a per-wave LDS ring).  A workgroup = 4 waves = 4 consecutive runs.
 #include "pv_device.hpp"
 #include "pv_kernels.h"
 
 namespace pv {
 
+// ------------------------------------------------------------------ shared frame code
+// Load frame t (window applied) into the pass-0 register layout: z[q] = (xw[2i], xw[2i+1]),
+// i = lane + 64 q.  Samples at index >= n read as 0.
+template <int L>
+__device__ __forceinline__ void load_frame_std(float2 (&z)[Geo<L>::E], const float* __restrict__ xc,
+                                               long long base, long long n, const float* __restrict__ win,
+                                               int aligned, int lane) {
+    constexpr int E = Geo<L>::E;
+    constexpr int N = 2 * L;
+    if (aligned && base + N <= n) {
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const int i = lane + 64 * q;
+            const float2 xv = *reinterpret_cast<const float2*>(xc + base + 2 * i);
+            const float2 wv = *reinterpret_cast<const float2*>(win + 2 * i);
+            z[q].x = xv.x * wv.x;
+            z[q].y = xv.y * wv.y;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const int i = lane + 64 * q;
+            const long long s = base + 2 * i;
+            const float x0 = (s < n) ? xc[s] : 0.0f;
+            const float x1 = (s + 1 < n) ? xc[s + 1] : 0.0f;
+            z[q].x = x0 * win[2 * i];
+            z[q].y = x1 * win[2 * i + 1];
+        }
+    }
+}
+
+// Real-FFT split of bin k (0 <= k <= L) from the natural-order L-point transform in tile.
+template <int L>
+__device__ __forceinline__ float2 real_split(const float2* tile, const float2* __restrict__ tws, int k) {
+    using G_ = Geo<L>;
+    const float2 A = tile[G_::pad(k & (L - 1))];
+    const float2 Bz = tile[G_::pad((L - k) & (L - 1))];
+    const float er = 0.5f * (A.x + Bz.x);
+    const float ei = 0.5f * (A.y - Bz.y);
+    const float orr = 0.5f * (A.y + Bz.y);
+    const float oi = 0.5f * (Bz.x - A.x);
+    const float2 tw = tws[k];
+    float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
+    float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
+    if (k == 0 || k == L) Xi = 0.0f;
+    return make_float2(Xr, Xi);
+}
+
+// All bins of a lane at once (LDS reads batched ahead of the arithmetic).
+template <int L>
+__device__ __forceinline__ void real_split_all(const float2* tile, const float2* twsl, int lane,
+                                               float2 (&X)[Geo<L>::E + 1]) {
+    using G_ = Geo<L>;
+    constexpr int E = G_::E;
+    float2 A[E + 1], Bz[E + 1], tw[E + 1];
+#pragma unroll
+    for (int i = 0; i <= E; ++i) {
+        const int k = (i == E) ? ((lane == 0) ? L : 0) : lane + 64 * i;
+        A[i] = tile[G_::pad(k & (L - 1))];
+        Bz[i] = tile[G_::pad((L - k) & (L - 1))];
+        tw[i] = twsl[k];
+    }
+#pragma unroll
+    for (int i = 0; i <= E; ++i) {
+        const int k = (i == E) ? ((lane == 0) ? L : 0) : lane + 64 * i;
+        const float er = 0.5f * (A[i].x + Bz[i].x);
+        const float ei = 0.5f * (A[i].y - Bz[i].y);
+        const float orr = 0.5f * (A[i].y + Bz[i].y);
+        const float oi = 0.5f * (Bz[i].x - A[i].x);
+        float Xr = er + __builtin_fmaf(orr, tw[i].x, -(oi * tw[i].y));
+        float Xi = ei + __builtin_fmaf(orr, tw[i].y, oi * tw[i].x);
+        if (k == 0 || k == L) Xi = 0.0f;
+        X[i] = make_float2(Xr, Xi);
+    }
+}
+
+// bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
+#define PV_FOR_BINS(E_, lane_, ...)                              \
+    _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \
+        if (i == (E_) && (lane_) != 0) break;                    \
+        const int k = (i == (E_)) ? 64 * (E_) : (lane_) + 64 * i; \
+        (void)k;                                                 \
+        __VA_ARGS__                                              \
+    }
+
 // ------------------------------------------------------------------ K1 STANDARD
+// One wave = one run of F consecutive frames (plus the halo frame t0-1, transformed only
+// for its phase).  The unwrap decision m(t) = f(phi[t], phi[t-1]) is accumulated in
+// registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
 template <int L>
 __global__ __launch_bounds__(256) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
+    constexpr int B = L + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* twl = reinterpret_cast<float2*>(smem);
-    float2* tiles = twl + L;
-    float* phiring = reinterpret_cast<float*>(tiles + 4 * G_::TILE);
+    float2* twl = reinterpret_cast<float2*>(smem);   // L   stage-major twiddles
+    float2* twsl = twl + L;                           // L+1 split twiddles (+1 pad)
+    float2* tiles = twsl + (L + 2);                   // 4 x TILE
+    float* winl = reinterpret_cast<float*>(tiles + 4 * G_::TILE);  // N
+    float* ekl = winl + N;                            // B
     const int BP = p.bins_pad;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int run = blockIdx.x, c = blockIdx.y;
+    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
+    for (int i = tid; i < B; i += 256) { twsl[i] = p.tws[i]; ekl[i] = p.ek[i]; }
+    for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
+    __syncthreads();
+    const int run = blockIdx.x * 4 + w, c = blockIdx.y;
+    if (run >= p.nruns) return;
     const int t0 = run * p.F;
     const int nfr = min(p.F, p.frames - t0);
-    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
-    __syncthreads();
 
     float2* tile = tiles + w * G_::TILE;
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
-    int sacc[E + 1];
-#pragma unroll
-    for (int i = 0; i <= E; ++i) sacc[i] = 0;
+    float phprev[E + 1];
+    int sacc[E + 1], m0[E + 1];
+    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; m0[i] = 0; })
 
-    const int rounds = (nfr + 3) >> 2;
-    for (int r = 0; r < rounds; ++r) {
-        const int u = 4 * r + w;
-        const bool valid = u < nfr;
+    // raw samples of the next frame are loaded one frame ahead (software pipeline)
+    auto fetch = [&](int t, float2 (&xr)[E]) {
+        const long long base = (long long)t * p.hop;
+        if (p.aligned && base + N <= p.n) {
+#pragma unroll
+            for (int q = 0; q < E; ++q)
+                xr[q] = *reinterpret_cast<const float2*>(xc + base + 2 * (lane + 64 * q));
+        } else {
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const long long s = base + 2 * (lane + 64 * q);
+                xr[q].x = (s < p.n) ? xc[s] : 0.0f;
+                xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
+            }
+        }
+    };
+    const int u0 = (t0 > 0) ? -1 : 0;
+    float2 xr[E];
+    fetch(t0 + u0, xr);
+    for (int u = u0; u < nfr; ++u) {
         const int t = t0 + u;
-        float phi[E + 1];
-        if (valid) {
-            float2 z[E];
-            const long long base = (long long)t * p.hop;
-            if (base + N <= p.n && p.aligned) {
+        float2 z[E];
 #pragma unroll
-                for (int q = 0; q < E; ++q) {
-                    const int i = lane + 64 * q;
-                    const float2 xv = *reinterpret_cast<const float2*>(xc + base + 2 * i);
-                    const float2 wv = *reinterpret_cast<const float2*>(p.win + 2 * i);
-                    z[q].x = xv.x * wv.x;
-                    z[q].y = xv.y * wv.y;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < E; ++q) {
-                    const int i = lane + 64 * q;
-                    const long long s = base + 2 * i;
-                    const float x0 = (s < p.n) ? xc[s] : 0.0f;
-                    const float x1 = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
-                    z[q].x = x0 * p.win[2 * i];
-                    z[q].y = x1 * p.win[2 * i + 1];
-                }
-            }
-            fft_run<L, false>(z, tile, twl, lane);
+        for (int q = 0; q < E; ++q) {
+            const float2 wv = reinterpret_cast<const float2*>(winl)[lane + 64 * q];
+            z[q].x = xr[q].x * wv.x;
+            z[q].y = xr[q].y * wv.y;
+        }
+        if (u + 1 < nfr) fetch(t + 1, xr);
+        fft_run<L, false>(z, tile, twl, lane);
+        float2 X[E + 1];
+        real_split_all<L>(tile, twsl, lane, X);
+        wave_lds_sync();  // tile reads done before the next frame's pass_store
+        float ph[E + 1];
+        PV_FOR_BINS(E, lane, { ph[i] = atan2_pv(X[i].y, X[i].x); })
+        if (u >= 0) {
             float2* srow = specc + (long long)t * p.spec_stride;
-#pragma unroll
-            for (int i = 0; i <= E; ++i) {
-                if (i == E && lane != 0) break;
-                const int k = (i == E) ? L : lane + 64 * i;
-                const float2 A = tile[G_::pad(k & (L - 1))];
-                const float2 Bz = tile[G_::pad((L - k) & (L - 1))];
-                const float er = 0.5f * (A.x + Bz.x);
-                const float ei = 0.5f * (A.y - Bz.y);
-                const float orr = 0.5f * (A.y + Bz.y);
-                const float oi = 0.5f * (Bz.x - A.x);
-                const float2 tw = p.tws[k];
-                float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
-                float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
-                if (k == 0 || k == L) Xi = 0.0f;
-                const float mag = __builtin_sqrtf(__builtin_fmaf(Xr, Xr, Xi * Xi));
-                const float ph = atan2_pv(Xi, Xr);
-                phi[i] = ph;
-                srow[k] = make_float2(mag, ph);
-                phiring[(u % 5) * BP + k] = ph;
-            }
+            PV_FOR_BINS(E, lane, {
+                const float mag = __builtin_sqrtf(__builtin_fmaf(X[i].x, X[i].x, X[i].y * X[i].y));
+                srow[k] = make_float2(mag, ph[i]);
+                const int m = unwrap_count(ph[i], phprev[i], ekl[k]);
+                m0[i] = (u == 0) ? m : m0[i];
+                sacc[i] += (u == 0) ? 0 : m;
+            })
         }
-        __syncthreads();
-        if (valid && u > 0) {
-            const float* prev = phiring + ((u + 4) % 5) * BP;
-#pragma unroll
-            for (int i = 0; i <= E; ++i) {
-                if (i == E && lane != 0) break;
-                const int k = (i == E) ? L : lane + 64 * i;
-                sacc[i] += unwrap_count(phi[i], prev[k], p.ek[k]);
-            }
-        }
-        __syncthreads();
+        PV_FOR_BINS(E, lane, { phprev[i] = ph[i]; })
     }
     if (p.runsum != nullptr) {
-        int* sred = reinterpret_cast<int*>(tiles);  // tiles are free now
-#pragma unroll
-        for (int i = 0; i <= E; ++i) {
-            if (i == E && lane != 0) break;
-            const int k = (i == E) ? L : lane + 64 * i;
-            sred[w * BP + k] = sacc[i];
-        }
-        __syncthreads();
-        int* dst = p.runsum + ((long long)c * p.nruns + run) * BP;
-        for (int k = tid; k <= L; k += 256)
-            dst[k] = sred[k] + sred[BP + k] + sred[2 * BP + k] + sred[3 * BP + k];
+        int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * BP;
+        PV_FOR_BINS(E, lane, { dst[k] = sacc[i]; dst[BP + k] = m0[i]; })
     }
 }
 
@@ -135,16 +204,17 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     float2* tiles = twl + L;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int run = blockIdx.x, c = blockIdx.y;
-    const int t0 = run * p.F;
-    const int nfr = min(p.F, p.frames - t0);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
     __syncthreads();
+    const int run = blockIdx.x * 4 + w, c = blockIdx.y;
+    if (run >= p.nruns) return;
+    const int t0 = run * p.F;
+    const int nfr = min(p.F, p.frames - t0);
     float2* tile = tiles + w * G_::TILE;
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
 
-    for (int u = w; u < nfr; u += 4) {
+    for (int u = 0; u < nfr; ++u) {
         const int t = t0 + u;
         const long long base = (long long)t * p.hop;
         float2 z[E];
@@ -167,30 +237,21 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
         }
         fft_run<L, false>(z, tile, twl, lane);
         float2* srow = specc + (long long)t * p.spec_stride;
-#pragma unroll
-        for (int i = 0; i <= E; ++i) {
-            if (i == E && lane != 0) break;
-            const int k = (i == E) ? L : lane + 64 * i;
-            const float2 A = tile[G_::pad(k & (L - 1))];
-            const float2 Bz = tile[G_::pad((L - k) & (L - 1))];
-            const float er = 0.5f * (A.x + Bz.x);
-            const float ei = 0.5f * (A.y - Bz.y);
-            const float orr = 0.5f * (A.y + Bz.y);
-            const float oi = 0.5f * (Bz.x - A.x);
-            const float2 tw = p.tws[k];
-            const float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
-            float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
-            if (k == 0 || k == L) Xi = 0.0f;
-            const float mag = __builtin_sqrtf(Xr * Xr + Xi * Xi);
-            float ph = atanf(Xi / Xr);
-            if (Xr == 0.0f && Xi == 0.0f) ph = p.nan_faithful ? __builtin_nanf("") : 0.0f;
+        PV_FOR_BINS(E, lane, {
+            const float2 X = real_split<L>(tile, p.tws, k);
+            const float mag = __builtin_sqrtf(X.x * X.x + X.y * X.y);
+            float ph = atanf(X.y / X.x);
+            if (X.x == 0.0f && X.y == 0.0f) ph = p.nan_faithful ? __builtin_nanf("") : 0.0f;
             srow[k] = make_float2(mag, ph);
             if (k != 0 && k != L) srow[2 * N - k] = make_float2(mag, -ph);
-        }
+        })
+        wave_lds_sync();
     }
 }
 
 // ------------------------------------------------------------------ K2 scans
+// run record from an existing spectrum (pv_resynthesis path): S (pairs inside the run)
+// and m0 = m(t0) against phi[t0-1] (0 before the first frame).
 __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int run = blockIdx.y, c = blockIdx.z;
@@ -199,201 +260,193 @@ __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
     const int nfr = min(p.F, p.frames - t0);
     const float2* s = p.spec + (long long)c * p.ld_spec + (long long)t0 * p.spec_stride + k;
     const float e = p.ek[k];
-    float prev = s[0].y;
+    float prev = (t0 > 0) ? s[-(long long)p.spec_stride].y : 0.0f;
+    float ph = s[0].y;
+    const int m0 = unwrap_count(ph, prev, e);
+    prev = ph;
     int acc = 0;
     for (int u = 1; u < nfr; ++u) {
-        const float ph = s[(long long)u * p.spec_stride].y;
+        ph = s[(long long)u * p.spec_stride].y;
         acc += unwrap_count(ph, prev, e);
         prev = ph;
     }
-    p.runsum[((long long)c * p.nruns + run) * p.bins_pad + k] = acc;
+    int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * p.bins_pad;
+    dst[k] = acc;
+    dst[p.bins_pad + k] = m0;
 }
 
+// carry[run] = M(t0) = sum over earlier runs of (m0 + S) + m0(run)
 __global__ __launch_bounds__(256) void k_carry(ScanParams p) {
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int c = blockIdx.y;
     if (k > p.L) return;
-    const float2* s = p.spec + (long long)c * p.ld_spec + k;
-    const float e = p.ek[k];
-    const int* rs = p.runsum + (long long)c * p.nruns * p.bins_pad + k;
-    int* cr = p.carry + (long long)c * p.nruns * p.bins_pad + k;
+    const int BP = p.bins_pad;
+    const int* rs = p.runsum + (long long)c * p.nruns * 2 * BP + k;
+    int* cr = p.carry + (long long)c * p.nruns * BP + k;
     int M = 0;
-    for (int run = 0; run < p.nruns; ++run) {
-        const long long t0 = (long long)run * p.F;
-        const float ph0 = s[t0 * p.spec_stride].y;
-        const float php = (t0 > 0) ? s[(t0 - 1) * p.spec_stride].y : 0.0f;
-        M += unwrap_count(ph0, php, e);
-        cr[(long long)run * p.bins_pad] = M;
-        M += rs[(long long)run * p.bins_pad];
+    int run = 0;
+    for (; run + 4 <= p.nruns; run += 4) {
+        int s[4], m[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s[j] = rs[(long long)(run + j) * 2 * BP];
+            m[j] = rs[(long long)(run + j) * 2 * BP + BP];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            M += m[j];
+            cr[(long long)(run + j) * BP] = M;
+            M += s[j];
+        }
+    }
+    for (; run < p.nruns; ++run) {
+        M += rs[(long long)run * 2 * BP + BP];
+        cr[(long long)run * BP] = M;
+        M += rs[(long long)run * 2 * BP];
     }
 }
 
 // ------------------------------------------------------------------ K3 synthesis
+// One wave = one run of F frames (virtually padded to F: frames >= `frames` are zero).
 // MODE 0: STANDARD — output phase rho*(phi + 2 pi (M_dec + (t+1) j_k)),
 //         Hann synthesis window with overlap normalisation folded into gain[].
 // MODE 1: REF_COMPAT — kernel.cu:352-432: x' = m cos(phi), y' = x' sin(phi), C2R N, /N,
-//         swap halves (rot = N/2), Hamming window (gain = w/N), overlap-add at out_hop.
+//         swap halves (rot = N/2), Hamming window (gain = w/N).
+// Overlap-add: per-wave LDS ring of N samples; a position is final once the frame that
+// starts after it has been added; final samples are stored straight to `out`.  After the
+// loop the three intra-workgroup seams are closed from the neighbours' rings (one
+// barrier); the workgroup's last tail goes to `tails` for k_seam.
 template <int L, int MODE>
 __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
+    constexpr int SPW = N / 64;  // samples per lane per frame
+    constexpr int B = L + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* twl = reinterpret_cast<float2*>(smem);
-    float2* tiles = twl + L;
-    float* ring = reinterpret_cast<float*>(tiles + 4 * G_::TILE);
-    float* phiring = ring + p.ring_size;         // 5 * BP   (MODE 0)
-    int* Mbase = reinterpret_cast<int*>(phiring + 5 * p.bins_pad);  // BP
-    int* mring = Mbase + p.bins_pad;                                 // 4 * BP
-    const int BP = p.bins_pad;
-    const int RMASK = p.ring_size - 1;
+    float2* twl = reinterpret_cast<float2*>(smem);                     // L
+    float2* twsl = twl + L;                                            // L (+2 pad)
+    float2* tiles = twsl + (L + 2);                                    // 4 x TILE
+    float* rings = reinterpret_cast<float*>(tiles + 4 * G_::TILE);    // 4 x N
+    float* gainl = rings + 4 * N;                                      // N
+    float* ekl = gainl + N;                                            // B (+pad)
+    unsigned* jkl = reinterpret_cast<unsigned*>(ekl + (B + 3));        // B (+pad)
+    int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
     const int hs = p.hs;
+    const int TL = N - hs;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int run = blockIdx.x, c = blockIdx.y;
-    const int t0 = run * p.F;
-    const int nfr = min(p.F, p.frames - t0);
-    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
-    for (int i = tid; i < p.ring_size; i += 256) ring[i] = 0.0f;
+    for (int i = tid; i < L; i += 256) { twl[i] = p.tw[i]; twsl[i] = p.tws[i]; }
+    for (int i = tid; i < N; i += 256) gainl[i] = p.gain[i];
     if (MODE == 0) {
-        const int* cr = p.carry + ((long long)c * p.nruns + run) * BP;
-        for (int k = tid; k <= L; k += 256) Mbase[k] = cr[k];
+        for (int i = tid; i < B; i += 256) {
+            ekl[i] = p.ek[i];
+            jkl[i] = p.jk_mod[i];
+            if (p.pitch) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
+        }
     }
+    float* ring = rings + w * N;
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) ring[lane + 64 * i] = 0.0f;
     __syncthreads();
 
+    const int c = blockIdx.y;
+    const int run = blockIdx.x * 4 + w;
+    const int t0 = run * p.F;
+    const int nfr = max(0, min(p.F, p.frames - t0));  // real frames of this wave's run
     float2* tile = tiles + w * G_::TILE;
     const float2* specc = p.spec + (long long)c * p.ld_spec;
     float* outc = p.out + (long long)c * p.ldo;
     const long long obase = (long long)t0 * hs;
 
-    const int rounds = (nfr + 3) >> 2;
-    for (int r = 0; r < rounds; ++r) {
-        const int u = 4 * r + w;
-        const bool valid = u < nfr;
+    int M[E + 1];
+    float phprev[E + 1];
+    if (MODE == 0 && nfr > 0) {
+        const int* cr = p.carry + ((long long)c * p.nruns + run) * p.bins_pad;
+        PV_FOR_BINS(E, lane, { M[i] = cr[k]; phprev[i] = 0.0f; })
+    }
+
+    float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
+    if (nfr > 0) {
+        const float2* srow = specc + (long long)t0 * p.spec_stride;
+        PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
+    }
+    for (int u = 0; u < p.F; ++u) {
         const int t = t0 + u;
-        float mag[E + 1], ph[E + 1];
-        if (valid) {
-            const float2* srow = specc + (long long)t * p.spec_stride;
-#pragma unroll
-            for (int i = 0; i <= E; ++i) {
-                if (i == E && lane != 0) break;
-                const int k = (i == E) ? L : lane + 64 * i;
-                const float2 v = srow[k];
-                mag[i] = v.x;
-                ph[i] = v.y;
+        if (u < nfr) {
+            float mag[E + 1], ph[E + 1];
+            PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
+            if (u + 1 < nfr) {
+                const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
+                PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
             }
-        }
-        float phc[E + 1];  // output phase (MODE 0) per analysis bin
-        if (MODE == 0) {
-            if (valid) {
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    phiring[(u % 5) * BP + k] = ph[i];
+            if (MODE == 0) {
+                const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
+                float phc[E + 1];
+                float ekv[E + 1];
+                unsigned jkv[E + 1];
+                PV_FOR_BINS(E, lane, { ekv[i] = ekl[k]; jkv[i] = jkl[k]; })
+                PV_FOR_BINS(E, lane, {
+                    const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
+                    M[i] += (u > 0) ? mm : 0;
+                    phprev[i] = ph[i];
+                })
+                // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
+                // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
+                const unsigned qq = (unsigned)p.q, pm = (unsigned)p.p_mod;
+                if (p.q_pow2) {
+                    PV_FOR_BINS(E, lane, {
+                        const unsigned x = pm * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
+                        phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * p.inv_q));
+                    })
+                } else {
+                    PV_FOR_BINS(E, lane, {
+                        int mdq = M[i] % (int)qq;
+                        mdq += (mdq < 0) ? (int)qq : 0;
+                        const unsigned x = pm * (unsigned)mdq + tq * jkv[i];
+                        phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x % qq) * p.inv_q));
+                    })
                 }
-            }
-            __syncthreads();
-            {
-                const float* prev = phiring + ((u + 4) % 5) * BP;
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    const int m = (valid && u > 0) ? unwrap_count(ph[i], prev[k], p.ek[k]) : 0;
-                    mring[w * BP + k] = m;
-                }
-            }
-            __syncthreads();
-            if (valid) {
-                const unsigned tq = (unsigned)((long long)(t + 1) % p.q);
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    int Md = Mbase[k];
-                    for (int ww = 0; ww <= w; ++ww) Md += mring[ww * BP + k];
-                    // (p*M_tot) mod q with M_tot = M_dec + (t+1) j_k, all reduced mod q
-                    int mdq;
-                    if (p.q_pow2) {
-                        mdq = Md & (int)(p.q - 1);  // two's complement: non-negative residue
-                    } else {
-                        mdq = Md % (int)p.q;
-                        if (mdq < 0) mdq += (int)p.q;
-                    }
-                    const unsigned long long x =
-                        (unsigned long long)p.p_mod * (unsigned long long)mdq +
-                        (unsigned long long)tq * (unsigned long long)p.jk_mod[k];
-                    const unsigned long long rr = p.q_pow2 ? (x & (unsigned long long)(p.q - 1))
-                                                           : (x % (unsigned long long)p.q);
-                    const float frac = (float)rr * p.inv_q;
-                    phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * frac);
-                }
-            }
-            __syncthreads();
-            if (w == 0) {
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    Mbase[k] += mring[k] + mring[BP + k] + mring[2 * BP + k] + mring[3 * BP + k];
-                }
-            }
-        }
-        if (valid) {
-            // polar -> rect into the tile (natural bin order, padded index)
-            if (MODE == 0 && p.pitch) {
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    tile[G_::pad(k)] = make_float2(mag[i], phc[i]);
-                }
-                wave_lds_sync();
-                float2 Y[E + 1];
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    const int s = p.src_first[k];
-                    float ms = 0.0f, pc = 0.0f;
-                    if (s >= 0) {
-                        const int cnt = p.src_cnt[k];
-                        pc = tile[G_::pad(s)].y;
-                        for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
-                    }
-                    float sn, cs;
-                    __builtin_sincosf(pc, &sn, &cs);
-                    Y[i] = make_float2(ms * cs, ms * sn);
-                }
-                wave_lds_sync();
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    float2 y = Y[i];
-                    if (k == 0 || k == L) y.y = 0.0f;
-                    tile[G_::pad(k)] = y;
+                if (p.pitch) {
+                    float2 Y[E + 1];
+                    PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
+                    wave_lds_sync();
+                    PV_FOR_BINS(E, lane, {
+                        const int s = srcl[k];
+                        float ms = 0.0f, pc = 0.0f;
+                        if (s >= 0) {
+                            const int cnt = srcl[B + k];
+                            pc = tile[G_::pad(s)].y;
+                            for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
+                        }
+                        float sn, cs;
+                        sincos_pv(pc, &sn, &cs);
+                        Y[i] = make_float2(ms * cs, ms * sn);
+                    })
+                    wave_lds_sync();
+                    PV_FOR_BINS(E, lane, {
+                        float2 y = Y[i];
+                        if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
+                        tile[G_::pad(k)] = y;
+                    })
+                } else {
+                    PV_FOR_BINS(E, lane, {
+                        float sn, cs;
+                        sincos_pv(phc[i], &sn, &cs);
+                        float2 y = make_float2(mag[i] * cs, mag[i] * sn);
+                        if (k == 0 || k == L) y.y = 0.0f;
+                        tile[G_::pad(k)] = y;
+                    })
                 }
             } else {
-#pragma unroll
-                for (int i = 0; i <= E; ++i) {
-                    if (i == E && lane != 0) break;
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    float2 y;
-                    if (MODE == 0) {
-                        float sn, cs;
-                        __builtin_sincosf(phc[i], &sn, &cs);
-                        y = make_float2(mag[i] * cs, mag[i] * sn);
-                    } else {
-                        float sn, cs;
-                        __builtin_sincosf(ph[i], &sn, &cs);
-                        const float xr = mag[i] * cs;   // kernel.cu:127
-                        y = make_float2(xr, xr * sn);   // kernel.cu:128 (uses updated x)
-                    }
+                PV_FOR_BINS(E, lane, {
+                    float sn, cs;
+                    sincos_pv(ph[i], &sn, &cs);
+                    const float xr = mag[i] * cs;                 // kernel.cu:127
+                    float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
                     if (k == 0 || k == L) y.y = 0.0f;
                     tile[G_::pad(k)] = y;
-                }
+                })
             }
             wave_lds_sync();
             // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
@@ -403,60 +456,55 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
                 const int i = lane + 64 * q;
                 const float2 A = tile[G_::pad(i)];
                 const float2 Bc = tile[G_::pad(L - i)];
-                const float fer = A.x + Bc.x, fei = A.y - Bc.y;    // A + conj(B)
-                const float dr = A.x - Bc.x, di = A.y + Bc.y;      // A - conj(B)
-                const float2 tw = p.tws[i];                        // e^{-2 pi i k/N}
-                // Fo = (A - conj B) * conj(tw)
-                const float For = __builtin_fmaf(dr, tw.x, di * tw.y);
+                const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
+                const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
+                const float2 tw = twsl[i];                       // e^{-2 pi i k/N}
+                const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
                 const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
                 z[q] = make_float2(fer - Foi, fei + For);
             }
             wave_lds_sync();
             fft_run<L, true>(z, tile, twl, lane);
-        }
-        __syncthreads();
-        // overlap-add of this round's frames into the LDS ring (fixed frame order)
-        {
-            const int base = 4 * r * hs;
-            const int span = 3 * hs + N;
-            for (int pp = tid; pp < span; pp += 256) {
-                const int pos = base + pp;
-                float sum = 0.0f;
+            // overlap-add the frame into the ring (lane-distinct positions)
+            const float* ty = reinterpret_cast<const float*>(tile);
 #pragma unroll
-                for (int ww = 0; ww < 4; ++ww) {
-                    const int uu = 4 * r + ww;
-                    const int pl = pos - uu * hs;
-                    if (uu < nfr && pl >= 0 && pl < N) {
-                        const int nn = (pl + p.rot) & (N - 1);
-                        const float* ty = reinterpret_cast<const float*>(tiles + ww * G_::TILE);
-                        const float yv = ty[2 * G_::pad(nn >> 1) + (nn & 1)];
-                        sum = __builtin_fmaf(yv, p.gain[pl], sum);
-                    }
-                }
-                ring[pos & RMASK] += sum;
+            for (int i = 0; i < SPW; ++i) {
+                const int n = lane + 64 * i;
+                const int nn = (n + p.rot) & (N - 1);
+                const float yv = ty[2 * G_::pad(nn >> 1) + (nn & 1)];
+                const int pos = (u * hs + n) & (N - 1);
+                ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
             }
+            wave_lds_sync();
         }
-        __syncthreads();
-        {
-            const int f0 = 4 * r * hs;
-            const int f1 = min(4 * r + 4, nfr) * hs;
-            for (int pos = f0 + tid; pos < f1; pos += 256) {
-                outc[obase + pos] = ring[pos & RMASK];
-                ring[pos & RMASK] = 0.0f;
-            }
+        // positions [u*hs, (u+1)*hs) are final for this run
+        for (int j = lane; j < hs; j += 64) {
+            const int pl = u * hs + j;
+            const int slot = pl & (N - 1);
+            const float v = ring[slot];
+            ring[slot] = 0.0f;
+            if (obase + pl < p.out_len) outc[obase + pl] = v;
         }
+        wave_lds_sync();
     }
     __syncthreads();
-    // tail: [nfr*hs, nfr*hs + N - hs)
-    {
-        const int tl = N - hs;
-        const bool last = (t0 + nfr >= p.frames);
-        float* tdst = p.tails + ((long long)c * p.nruns + run) * p.tail_len;
-        for (int j = tid; j < tl; j += 256) {
-            const int pos = nfr * hs + j;
-            const float v = ring[pos & RMASK];
+    // seams: run w's tail (ring positions [F*hs, F*hs + TL)) overlaps run w+1's head
+    if (w > 0) {
+        const float* prev = rings + (w - 1) * N;
+        for (int j = lane; j < TL; j += 64) {
+            const long long gp = obase + j;
+            if (gp < p.out_len) outc[gp] += prev[(p.F * hs + j) & (N - 1)];
+        }
+    }
+    if (w == 3) {
+        const int nwg = (p.nruns + 3) / 4;
+        const bool last = (blockIdx.x + 1 >= nwg);
+        float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len;
+        for (int j = lane; j < TL; j += 64) {
+            const float v = ring[(p.F * hs + j) & (N - 1)];
             if (last) {
-                if (obase + pos < p.out_len) outc[obase + pos] = v;
+                const long long gp = obase + (long long)p.F * hs + j;
+                if (gp < p.out_len) outc[gp] = v;
             } else {
                 tdst[j] = v;
             }
@@ -465,6 +513,7 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
 }
 
 // ------------------------------------------------------------------ K4 seam
+// adds each workgroup's last tail into the next workgroup's head (and ola_in at 0)
 __global__ __launch_bounds__(256) void k_seam(SeamParams p) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     const int b = blockIdx.y, c = blockIdx.z;
@@ -473,25 +522,25 @@ __global__ __launch_bounds__(256) void k_seam(SeamParams p) {
     if (b == 0) {
         if (p.ola_in != nullptr && j < p.out_len) outc[j] += p.ola_in[(long long)c * p.ld_ola + j];
     } else {
-        const long long pos = (long long)b * p.F * p.hs + j;
+        const long long pos = (long long)b * 4 * p.F * p.hs + j;
         if (pos < p.out_len)
-            outc[pos] += p.tails[((long long)c * p.nruns + (b - 1)) * p.tail_len + j];
+            outc[pos] += p.tails[((long long)c * p.nwg + (b - 1)) * p.tail_len + j];
     }
 }
 
 // ------------------------------------------------------------------ launchers
 template <int L>
-static size_t ana_lds_std(int bins_pad) {
-    return sizeof(float2) * (L + 4 * Geo<L>::TILE) + sizeof(float) * 5 * bins_pad;
+static size_t ana_lds_std(int) {
+    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + L + 1);
 }
 template <int L>
 static size_t ana_lds_compat() {
     return sizeof(float2) * (L + 4 * Geo<L>::TILE);
 }
 template <int L>
-static size_t syn_lds(int bins_pad, int ring) {
-    return sizeof(float2) * (L + 4 * Geo<L>::TILE) + sizeof(float) * ring +
-           sizeof(float) * 5 * bins_pad + sizeof(int) * 5 * bins_pad;
+static size_t syn_lds(int, int) {
+    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * 5 * (2 * L) +
+           sizeof(float) * 4 * (L + 1 + 3);
 }
 
 size_t synthesis_lds_bytes(int L, int bins_pad, int ring) {
@@ -516,7 +565,7 @@ size_t synthesis_lds_bytes(int L, int bins_pad, int ring) {
     }
 
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
-    dim3 grid(p.nruns, channels);
+    dim3 grid((p.nruns + 3) / 4, channels);
     PV_DISPATCH_L(L, {
         hipLaunchKernelGGL(k_std_analysis<LL>, grid, dim3(256), ana_lds_std<LL>(p.bins_pad), s, p);
     });
@@ -524,7 +573,7 @@ hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStrea
 }
 
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
-    dim3 grid(p.nruns, channels);
+    dim3 grid((p.nruns + 3) / 4, channels);
     PV_DISPATCH_L(L, {
         hipLaunchKernelGGL(k_compat_analysis<LL>, grid, dim3(256), ana_lds_compat<LL>(), s, p);
     });
@@ -544,23 +593,23 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
 }
 
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
-    dim3 grid(p.nruns, channels);
+    dim3 grid((p.nruns + 3) / 4, channels);
     if (mode == 0) {
         PV_DISPATCH_L(L, {
             hipLaunchKernelGGL((k_synthesis<LL, 0>), grid, dim3(256),
-                               syn_lds<LL>(p.bins_pad, p.ring_size), s, p);
+                               syn_lds<LL>(0, 0), s, p);
         });
     } else {
         PV_DISPATCH_L(L, {
             hipLaunchKernelGGL((k_synthesis<LL, 1>), grid, dim3(256),
-                               syn_lds<LL>(p.bins_pad, p.ring_size), s, p);
+                               syn_lds<LL>(0, 0), s, p);
         });
     }
     return hipGetLastError();
 }
 
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s) {
-    dim3 grid((p.tail_len + 255) / 256, p.nruns, channels);
+    dim3 grid((p.tail_len + 255) / 256, p.nwg, channels);
     hipLaunchKernelGGL(k_seam, grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Standalone driver for rocprofv3 counter passes: config 3 (1024 ch x 10 s, N=1024,
+hop=256, PV_STANDARD stretch 0.5) through pv_process, `--reps` times."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "phase-vocoder_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--channels", type=int, default=1024)
+    ap.add_argument("--effect", default="t")
+    ap.add_argument("--scale", type=float, default=0.5)
+    ap.add_argument("--N", type=int, default=1024)
+    ap.add_argument("--mode", default="standard")
+    args = ap.parse_args()
+    import torch
+    from bench import synth_channels_np
+    from pvamd import PhaseVocoder
+    n = 441000
+    pv = PhaseVocoder(args.N, args.effect, args.scale, 4, mode=args.mode,
+                      max_channels=args.channels, max_frames=2000)
+    # host-generated input + plain copy: no torch compute kernels in the profiled process
+    x = torch.from_numpy(synth_channels_np(args.channels, n, 20240)).to("cuda:0")
+    frames = pv.num_frames(n)
+    spec = pv.alloc_spec(args.channels, frames)
+    out = pv.alloc_out(args.channels, frames)
+    for _ in range(args.reps):
+        pv.process(x, spec=spec, out=out)
+    torch.cuda.synchronize()
+    print("done", frames)
+
+
+if __name__ == "__main__":
+    main()
