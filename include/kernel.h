@@ -1,0 +1,148 @@
+// kernel.h — header-only C++ drop-in for the reference's `namespace CudaPhase`
+// (karnel/kernel.h:13-21) on top of the libpv C-ABI (include/pv.h).
+//
+//   CudaPhase::pv_analysis_CUFFT(out2N, fft, in, interm, win, N)   kernel.cu:299-348
+//   CudaPhase::resynthesis_CUFFT(out, back, spec, win, N, hop)     kernel.cu:352-432
+//   CudaPhase::pv_analysis / resynthesis (hand-FFT variants)       kernel.cu:177-218, 262-288
+//   CudaPhase::test_overlap_add(...)                               kernel.cu:289-298
+//   CudaPhase::timer()  PerformanceTimer (karnel/common.h:27-113) on hipEvents
+//
+// The REF_COMPAT handles behind these free functions are created on first use per
+// (N, hop) and cached for the process lifetime; `win` must be the reference's window
+// (the handle holds an identical copy), `fft` / `intermediary` are unused.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "pv.h"
+
+namespace FFT {
+namespace Common {
+// karnel/common.h:27-113: cpu timer (chrono) + gpu timer (events)
+class PerformanceTimer {
+   public:
+    PerformanceTimer() {
+        (void)hipEventCreate(&start_);
+        (void)hipEventCreate(&stop_);
+    }
+    ~PerformanceTimer() {
+        (void)hipEventDestroy(start_);
+        (void)hipEventDestroy(stop_);
+    }
+    void startCpuTimer() { cpu0_ = std::chrono::high_resolution_clock::now(); }
+    void endCpuTimer() {
+        auto t = std::chrono::high_resolution_clock::now();
+        prev_cpu_ms_ = std::chrono::duration<float, std::milli>(t - cpu0_).count();
+    }
+    void startGpuTimer() { (void)hipEventRecord(start_); }
+    void endGpuTimer() {
+        (void)hipEventRecord(stop_);
+        (void)hipEventSynchronize(stop_);
+        (void)hipEventElapsedTime(&prev_gpu_ms_, start_, stop_);
+    }
+    float getCpuElapsedTimeForPreviousOperation() { return prev_cpu_ms_; }
+    float getGpuElapsedTimeForPreviousOperation() { return prev_gpu_ms_; }
+
+   private:
+    hipEvent_t start_{}, stop_{};
+    std::chrono::high_resolution_clock::time_point cpu0_{};
+    float prev_cpu_ms_ = 0.f, prev_gpu_ms_ = 0.f;
+};
+}  // namespace Common
+}  // namespace FFT
+
+namespace CudaPhase {
+
+inline FFT::Common::PerformanceTimer& timer() {
+    static FFT::Common::PerformanceTimer t;
+    return t;
+}
+
+namespace detail {
+inline void check(pv_status st, const char* msg) {  // checkCUDAError_ (io.cpp:115-124)
+    if (st != PV_OK) {
+        std::fprintf(stderr, "Cuda error: %s: %s.\n", msg, pv_last_error());
+        std::exit(EXIT_FAILURE);
+    }
+}
+inline pv_handle* compat_handle(int N, int hop) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, pv_handle*> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({N, hop});
+    if (it != cache.end()) return it->second;
+    pv_config cfg{};
+    cfg.n_samps = N;
+    cfg.hop_div = (hop > 0 && N % hop == 0) ? N / hop : 2;
+    cfg.effect = PV_TIME_SHIFT;
+    cfg.scale = (hop > 0 && N % hop == 0) ? 1.0f : (float)hop / (float)(N / 2);
+    cfg.mode = PV_MODE_REF_COMPAT;
+    cfg.max_channels = 1;
+    cfg.max_frames = 1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    cfg.device = dev;
+    pv_handle* h = nullptr;
+    check(pv_create(&cfg, &h), "pv_create");
+    cache[{N, hop}] = h;
+    return h;
+}
+inline int spec_stride(pv_handle* h) {
+    pv_info info{};
+    pv_get_info(h, &info);
+    return info.spec_stride;
+}
+}  // namespace detail
+
+// kernel.cu:299-348
+inline void pv_analysis_CUFFT(float2* output, float2* fft, float* input, float* intermediary,
+                              float* win, int N) {
+    (void)fft;
+    (void)intermediary;
+    (void)win;
+    timer().startGpuTimer();
+    pv_handle* h = detail::compat_handle(N, N / 2);
+    detail::check(pv_analysis(h, input, N, N, 1, 1, (pv_float2*)output, detail::spec_stride(h), nullptr),
+                  "pv_analysis_CUFFT");
+    timer().endGpuTimer();
+}
+
+// kernel.cu:352-432 (output = frame + backFrame[hop..N) shifted to the front)
+inline void resynthesis_CUFFT(float* output, float* backFrame, float2* frontFrame, float* win,
+                              int N, int hopSize) {
+    (void)win;
+    timer().startGpuTimer();
+    pv_handle* h = detail::compat_handle(N, hopSize);
+    detail::check(pv_resynthesis(h, (const pv_float2*)frontFrame, detail::spec_stride(h), 1, 1,
+                                 backFrame + hopSize, N, output, N, nullptr),
+                  "resynthesis_CUFFT");
+    timer().endGpuTimer();
+}
+
+// kernel.cu:177-218 / 262-288: the hand-FFT variants compute the same contract here
+inline void pv_analysis(float2* output, float2* fft, float* input, float* intermediary, float* win,
+                        int N) {
+    pv_analysis_CUFFT(output, fft, input, intermediary, win, N);
+}
+inline void resynthesis(float* output, float* backFrame, float2* frontFrame, float2* intermediary,
+                        float* win, int N, int hopSize) {
+    (void)intermediary;
+    resynthesis_CUFFT(output, backFrame, frontFrame, win, N, hopSize);
+}
+
+// kernel.cu:289-298: window, shift, unshift, window, overlap-add (identity processing)
+inline void test_overlap_add(float* input, float* output, float* intermediary, float* backFrame,
+                             float* win, int N, int hopSize) {
+    (void)intermediary;
+    detail::check(pv_test_overlap_add(input, win, backFrame, output, N, hopSize, nullptr),
+                  "test_overlap_add");
+    (void)hipStreamSynchronize(nullptr);
+}
+
+}  // namespace CudaPhase

@@ -61,7 +61,7 @@ typedef enum pv_mode {
 } pv_mode;
 
 typedef struct pv_config {
-    int n_samps;      /* N, window length: power of 2; STANDARD 256..4096, REF_COMPAT 128..2048 */
+    int n_samps;      /* N, window length: power of 2 in [256, 2048] (both modes)       */
     int hop_div;      /* hop = N / hop_div (phaseVocoder.h:79 4th argument is a divisor)  */
     int effect;       /* pv_effect                                                      */
     float scale;      /* TIME_SHIFT: out_hop = (int)(scale*hop); PITCH_SHIFT: pitch ratio */
@@ -111,6 +111,11 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);
+
+/* kernel.cu:289-298 (OVERLAPTEST, main.cpp:156-202): identity processing of one frame,
+ * out[k] = win[k]^2 * in[k] + (k + hop < N ? back[k + hop] : 0).  Device pointers. */
+pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,
+                              int n, int hop, void* stream);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py). */
 pv_status pv_profile_enable(pv_handle* h, int enable);

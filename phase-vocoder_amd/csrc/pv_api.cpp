@@ -346,8 +346,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if (cfg->hop_div <= 0 || N / cfg->hop_div <= 0) return fail(PV_ERR_ARG, "bad hop_div");
     if (cfg->max_channels < 0 || cfg->max_frames < 0) return fail(PV_ERR_ARG, "negative capacity");
     if (!(cfg->scale > 0.0f) || !std::isfinite(cfg->scale)) return fail(PV_ERR_ARG, "scale must be > 0");
-    if (cfg->mode == PV_MODE_STANDARD && (N < 256 || N > 4096))
-        return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: n_samps in [256, 4096]");
+    if (cfg->mode == PV_MODE_STANDARD && (N < 256 || N > 2048))
+        return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: n_samps in [256, 2048]");
     if (cfg->mode == PV_MODE_REF_COMPAT && (N < 256 || N > 2048))
         return fail(PV_ERR_UNSUPPORTED, "REF_COMPAT mode: n_samps in [256, 2048]");
 
@@ -532,6 +532,14 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
     if (st != PV_OK) return st;
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
+}
+
+pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,
+                              int n, int hop, void* stream) {
+    if (!in || !win || !back || !out || n <= 0 || hop < 0) return fail(PV_ERR_ARG, "bad argument");
+    hipError_t e = pv::launch_overlap_test(in, win, back, out, n, hop, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("test_overlap_add: ") + hipGetErrorString(e));
+    return PV_OK;
 }
 
 pv_status pv_profile_enable(pv_handle* h, int enable) {

@@ -72,5 +72,7 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
 size_t synthesis_lds_bytes(int L, int bins_pad, int ring);
+hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,
+                               int n, int hop, hipStream_t s);
 
 }  // namespace pv

@@ -528,6 +528,27 @@ __global__ __launch_bounds__(256) void k_seam(SeamParams p) {
     }
 }
 
+// ------------------------------------------------------------------ OVERLAPTEST
+// kernel.cu:289-298: cudaWindow, cufftShift (out-of-place), cufftShift (in place),
+// cudaWindow, cudaOverlapAdd -> out[k] = w[k]^2 x[k] + back[k + hop]
+__global__ __launch_bounds__(256) void k_overlap_test(const float* __restrict__ in,
+                                                       const float* __restrict__ win,
+                                                       const float* __restrict__ back,
+                                                       float* __restrict__ out, int n, int hop) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    float v = in[k] * win[k];
+    v = v * win[k];
+    if (k + hop < n) v += back[k + hop];
+    out[k] = v;
+}
+
+hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,
+                               int n, int hop, hipStream_t s) {
+    hipLaunchKernelGGL(k_overlap_test, dim3((n + 255) / 256), dim3(256), 0, s, in, win, back, out, n, hop);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers
 template <int L>
 static size_t ana_lds_std(int) {

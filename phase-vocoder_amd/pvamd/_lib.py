@@ -73,6 +73,8 @@ def lib():
     L.pv_resynthesis.restype = i
     L.pv_process.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, vp]
     L.pv_process.restype = i
+    L.pv_test_overlap_add.argtypes = [vp, vp, vp, vp, i, i, vp]
+    L.pv_test_overlap_add.restype = i
     L.pv_profile_enable.argtypes = [vp, i]
     L.pv_profile_enable.restype = i
     L.pv_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),

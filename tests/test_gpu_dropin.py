@@ -1,0 +1,123 @@
+"""GPU tests of the drop-in surface: the C++ driver pv_main (main.cpp's offline loop on
+the phaseVocoder.h drop-in), the Python mirror's per-frame reference methods, and the
+OVERLAPTEST identity path — each checked against the CPU oracle."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import pvref
+from conftest import GOLDEN, ROOT
+from pvamd import REF_COMPAT, STANDARD, TIME_SHIFT, PhaseVocoder, wav
+
+pytestmark = pytest.mark.gpu
+
+PV_MAIN = os.path.join(ROOT, "phase-vocoder_amd", "build", "pv_main")
+
+
+def write_pcm16(path, x):
+    """x = int16/32768 values (exact): write them back bit-exactly as mono 16-bit PCM."""
+    ints = np.round(np.asarray(x, np.float64) * 32768.0).astype("<i2")
+    body = ints.tobytes()
+    hdr = b"RIFF" + struct.pack("<i", 36 + len(body)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<ihhiihh", 16, 1, 1, 44100, 88200, 2, 16)
+    hdr += b"data" + struct.pack("<i", len(body))
+    open(path, "wb").write(hdr + body)
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+@pytest.fixture(scope="module")
+def sine440(tmp_path_factory):
+    x = np.load(os.path.join(GOLDEN, "sine440_ch0_32768.npy"))
+    p = str(tmp_path_factory.mktemp("wav") / "sine440.wav")
+    write_pcm16(p, x)
+    return p, x
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_pv_main_ref_compat_config1_geometry(cuda, sine440, tmp_path, batched):
+    """config 1 geometry (N=1024, hop 256, scale 1, REF_COMPAT) through the C++ driver."""
+    path, x = sine440
+    out_wav, dump = str(tmp_path / "out.wav"), str(tmp_path / "out.f32")
+    cmd = [PV_MAIN, path, "t", out_wav, "--N", "1024", "--hopdiv", "4", "--dump-f32", dump]
+    if batched:
+        cmd.append("--batched")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(dump, np.float32)
+    ref = pvref.compat_process(x, 1024, 4)
+    n_emit = (len(x) // 256) * 256  # main.cpp:266 emits floor(n/outHop) hops
+    assert len(got) >= n_emit
+    assert rms(got[:n_emit], ref[:n_emit]) <= 1e-5
+    s, sr, bits = wav.load(out_wav)
+    assert s.shape == (2, len(x)) and bits == 16 and sr == 44100
+    assert np.array_equal(s[0], s[1])  # R duplicates L (main.cpp:288-289)
+    q = np.trunc(np.clip(ref[:n_emit], -1, 1) * 32767) / 32768.0
+    assert np.max(np.abs(s[0, :n_emit] - q)) <= 1.01 / 32768  # at most 1 LSB from rounding
+
+
+def test_pv_main_standard_batched(cuda, sine440, tmp_path):
+    path, x = sine440
+    dump = str(tmp_path / "o.f32")
+    r = subprocess.run([PV_MAIN, path, "p", str(tmp_path / "o.wav"), "--N", "1024", "--hopdiv", "4",
+                        "--scale", "1.5", "--mode", "std", "--batched", "--dump-f32", dump],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(dump, np.float32)
+    ref = pvref.std_process(x, 1024, 4, ord("p"), 1.5)
+    assert rms(got, ref[:len(got)]) <= 1e-5
+
+
+def test_python_mirror_per_frame_loop_matches_batched(cuda):
+    """main.cpp's per-frame loop written with the reference method names."""
+    import torch
+    x = np.load(os.path.join(GOLDEN, "sine440_ch0_32768.npy"))[:8192]
+    N, hd = 1024, 4
+    pv = PhaseVocoder(N, TIME_SHIFT, 1.0, hd, mode=REF_COMPAT, max_frames=64)
+    hop = pv.hopSize
+    d_input = torch.zeros(len(x) + 2 * N, device="cuda")
+    d_input[:len(x)] = torch.from_numpy(x).cuda()
+    nspec = len(x) // hop + 1
+    d_output = torch.zeros((nspec, pv.spec_stride, 2), device="cuda")
+    for i in range(0, len(x) - hop, hop):                       # main.cpp:231
+        pv.analysis_CUFFT(d_input[i:], d_output[i // hop])
+    back = torch.zeros(N, device="cuda")
+    final = torch.empty(N, device="cuda")
+    emitted = []
+    for i in range(len(x) // pv.outHopSize):                    # main.cpp:266
+        pv.resynthesis_CUFFT(back, d_output[min(i, nspec - 1)], final)
+        back.copy_(final)
+        emitted.append(back[:pv.outHopSize].cpu().numpy().copy())
+    got = np.concatenate(emitted)
+    ref = pvref.compat_process(x, N, hd)
+    assert rms(got, ref[:len(got)]) <= 1e-5
+    out, _ = PhaseVocoder(N, TIME_SHIFT, 1.0, hd, mode=REF_COMPAT, max_frames=64).process(
+        torch.from_numpy(x).cuda())
+    assert rms(got, out.cpu().numpy()[0][:len(got)]) <= 1e-6
+
+
+def test_overlap_test_identity(cuda):
+    """OVERLAPTEST (main.cpp:156-202, kernel.cu:289-298): out = w^2 x + back[hop:]."""
+    import ctypes
+    import torch
+    from pvamd import _lib
+    from pvamd.tables import hamming_ref
+    N, hop = 256, 128
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(N).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    w = hamming_ref(N)
+    dx, db, dw = (torch.from_numpy(v).cuda() for v in (x, b, w))
+    out = torch.empty(N, device="cuda")
+    st = _lib.lib().pv_test_overlap_add(ctypes.c_void_p(dx.data_ptr()), ctypes.c_void_p(dw.data_ptr()),
+                                        ctypes.c_void_p(db.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                        N, hop, None)
+    assert st == 0
+    ref = (x * w) * w
+    ref[:N - hop] += b[hop:]
+    assert np.allclose(out.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
