@@ -116,6 +116,11 @@ def main():
     pv = PhaseVocoder(N, TIME_SHIFT, scale, hop_div, mode=STANDARD, max_channels=C,
                       max_frames=pv_frames(n, N // hop_div), device=local)
     frames = pv.num_frames(n)
+    tables = None
+    if world > 1:  # init-time RCCL broadcast of rank 0's tables (north_star); not timed
+        from pvamd.dist import broadcast_tables
+        same = broadcast_tables(pv, src=0)
+        tables = {"bytes": int(pv.export_tables().numel()), "bit_identical_to_local": same}
     x = synth_channels(torch, C, n, 20240 + rank * C, dev)
     spec = pv.alloc_spec(C, frames)
     out = pv.alloc_out(C, frames)
@@ -192,6 +197,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
             "kernels": kernels,
+            "tables_broadcast": tables,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -112,6 +112,13 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);
 
+/* Constant tables of a handle (windows, gains, twiddles, unwrap tables, pitch map) as one
+ * device blob, so that one rank can build them and the others receive them over RCCL
+ * (DESIGN.md §6).  export with dst == NULL only reports *bytes.  import validates the
+ * blob's header against the handle's configuration and replaces the tables. */
+pv_status pv_export_tables(const pv_handle* h, void* dst, size_t cap, size_t* bytes, void* stream);
+pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* stream);
+
 /* kernel.cu:289-298 (OVERLAPTEST, main.cpp:156-202): identity processing of one frame,
  * out[k] = win[k]^2 * in[k] + (k + hop < N ? back[k + hop] : 0).  Device pointers. */
 pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,

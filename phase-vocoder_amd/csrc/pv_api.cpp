@@ -534,6 +534,96 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
 }
 
+namespace {
+struct TableBlobHeader {
+    uint32_t magic, version;
+    int32_t n_samps, hop, hs, mode, effect, pitch;
+    float scale;
+    int32_t L_ana, L_syn, bins;
+    uint32_t pad[4];
+};
+static_assert(sizeof(TableBlobHeader) == 64, "blob header is 64 bytes");
+constexpr uint32_t kBlobMagic = 0x50565442u;  // "PVTB"
+
+struct TableSeg {
+    void* ptr;
+    size_t bytes;
+};
+std::vector<TableSeg> table_segments(const pv_handle* h) {
+    const size_t N = h->N, B = h->bins;
+    return {{h->d_win, sizeof(float) * N},
+            {h->d_gain, sizeof(float) * N},
+            {h->d_tw_ana, sizeof(float2) * h->L_ana},
+            {h->d_tws_ana, sizeof(float2) * (h->L_ana + 1)},
+            {h->d_tw_syn, sizeof(float2) * h->L_syn},
+            {h->d_tws_syn, sizeof(float2) * (N / 2 + 1)},
+            {h->d_ek, sizeof(float) * B},
+            {h->d_jk_mod, sizeof(unsigned) * B},
+            {h->d_src_first, sizeof(int) * B},
+            {h->d_src_cnt, sizeof(int) * B}};
+}
+TableBlobHeader blob_header(const pv_handle* h) {
+    TableBlobHeader hd{};
+    hd.magic = kBlobMagic;
+    hd.version = 1;
+    hd.n_samps = h->N;
+    hd.hop = h->hop;
+    hd.hs = h->hs;
+    hd.mode = h->mode;
+    hd.effect = h->effect;
+    hd.pitch = h->pitch;
+    hd.scale = h->scale;
+    hd.L_ana = h->L_ana;
+    hd.L_syn = h->L_syn;
+    hd.bins = h->bins;
+    return hd;
+}
+size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+}  // namespace
+
+pv_status pv_export_tables(const pv_handle* h, void* dst, size_t cap, size_t* bytes, void* stream) {
+    if (!h || !bytes) return fail(PV_ERR_ARG, "null argument");
+    size_t total = sizeof(TableBlobHeader);
+    for (const auto& sg : table_segments(h)) total += align16(sg.bytes);
+    *bytes = total;
+    if (!dst) return PV_OK;
+    if (cap < total) return fail(PV_ERR_ARG, "export buffer too small");
+    DeviceGuard g(h->cfg.device);
+    hipStream_t s = (hipStream_t)stream;
+    static thread_local TableBlobHeader hd;  // host source must outlive the async copy
+    hd = blob_header(h);
+    PV_HIP(hipMemcpyAsync(dst, &hd, sizeof(hd), hipMemcpyHostToDevice, s));
+    size_t off = sizeof(TableBlobHeader);
+    for (const auto& sg : table_segments(h)) {
+        PV_HIP(hipMemcpyAsync((char*)dst + off, sg.ptr, sg.bytes, hipMemcpyDeviceToDevice, s));
+        off += align16(sg.bytes);
+    }
+    PV_HIP(hipStreamSynchronize(s));
+    return PV_OK;
+}
+
+pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* stream) {
+    if (!h || !src) return fail(PV_ERR_ARG, "null argument");
+    size_t total = 0;
+    pv_export_tables(h, nullptr, 0, &total, nullptr);
+    if (bytes != total) return fail(PV_ERR_ARG, "table blob size does not match this handle");
+    DeviceGuard g(h->cfg.device);
+    hipStream_t s = (hipStream_t)stream;
+    TableBlobHeader hd{};
+    PV_HIP(hipMemcpyAsync(&hd, src, sizeof(hd), hipMemcpyDeviceToHost, s));
+    PV_HIP(hipStreamSynchronize(s));
+    TableBlobHeader mine = blob_header(h);
+    if (std::memcmp(&hd, &mine, sizeof(hd)) != 0)
+        return fail(PV_ERR_ARG, "table blob was built for a different configuration");
+    size_t off = sizeof(TableBlobHeader);
+    for (const auto& sg : table_segments(h)) {
+        PV_HIP(hipMemcpyAsync(sg.ptr, (const char*)src + off, sg.bytes, hipMemcpyDeviceToDevice, s));
+        off += align16(sg.bytes);
+    }
+    PV_HIP(hipStreamSynchronize(s));
+    return PV_OK;
+}
+
 pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,
                               int n, int hop, void* stream) {
     if (!in || !win || !back || !out || n <= 0 || hop < 0) return fail(PV_ERR_ARG, "bad argument");

@@ -73,6 +73,10 @@ def lib():
     L.pv_resynthesis.restype = i
     L.pv_process.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, vp]
     L.pv_process.restype = i
+    L.pv_export_tables.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), vp]
+    L.pv_export_tables.restype = i
+    L.pv_import_tables.argtypes = [vp, vp, ctypes.c_size_t, vp]
+    L.pv_import_tables.restype = i
     L.pv_test_overlap_add.argtypes = [vp, vp, vp, vp, i, i, vp]
     L.pv_test_overlap_add.restype = i
     L.pv_profile_enable.argtypes = [vp, i]

@@ -189,6 +189,21 @@ class PhaseVocoder:
                                           _ptr(ola), self.nSamps, _ptr(output), self.nSamps,
                                           self._stream()), "resynthesis_CUFFT")
 
+    # -------------------------------------------------------------- shared tables
+    def export_tables(self):
+        """Constant tables as one uint8 CUDA tensor (header + windows + twiddles + ...)."""
+        torch = _torch()
+        n = ctypes.c_size_t()
+        self._call(self._L.pv_export_tables(self._h, None, 0, ctypes.byref(n), None), "pv_export_tables")
+        blob = torch.empty(n.value, dtype=torch.uint8, device=f"cuda:{self.device}")
+        self._call(self._L.pv_export_tables(self._h, _ptr(blob), n.value, ctypes.byref(n),
+                                            self._stream()), "pv_export_tables")
+        return blob
+
+    def import_tables(self, blob):
+        self._call(self._L.pv_import_tables(self._h, _ptr(blob), blob.numel(), self._stream()),
+                   "pv_import_tables")
+
     # -------------------------------------------------------------- profiling (bench.py)
     def profile(self, enable: bool = True):
         self._call(self._L.pv_profile_enable(self._h, 1 if enable else 0), "pv_profile_enable")

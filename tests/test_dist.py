@@ -1,0 +1,63 @@
+"""Multi-process (gloo, world_size 2, CPU) coverage of the sharded path: channel
+partition, the init-time table broadcast and the max-over-ranks timing reduction."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pvamd.dist import broadcast_blob, channel_shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # 1) shards: every channel exactly once
+        first, count = channel_shard(8192, world, rank)
+        got = torch.tensor([first, count])
+        allg = [torch.zeros(2, dtype=torch.long) for _ in range(world)]
+        dist.all_gather(allg, got)
+        # 2) table broadcast: rank 0's blob reaches every rank bit-exactly
+        g = torch.Generator().manual_seed(1234)
+        ref = torch.randint(0, 256, (12345,), dtype=torch.uint8, generator=g)
+        blob = ref.clone() if rank == 0 else torch.zeros_like(ref)
+        broadcast_blob(blob, src=0)
+        # 3) max over ranks of the step time
+        t = torch.tensor([1.0 + rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        results[rank] = (sorted(tuple(x.tolist()) for x in allg), bool(torch.equal(blob, ref)), float(t))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_shard_broadcast_timing(world):
+    port = _free_port()
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, port, results), nprocs=world, join=True)
+    for r in range(world):
+        shards, same, tmax = results[r]
+        assert same and tmax == float(world)
+        covered = []
+        for first, count in shards:
+            covered.extend(range(first, first + count))
+        assert covered == list(range(8192))
+
+
+def test_channel_shard_uneven():
+    parts = [channel_shard(10, 4, r) for r in range(4)]
+    assert parts == [(0, 3), (3, 3), (6, 2), (8, 2)]
+    with pytest.raises(ValueError):
+        channel_shard(10, 4, 4)

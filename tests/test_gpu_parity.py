@@ -104,3 +104,62 @@ def test_ref_compat_spectrum(cuda):
     assert np.max(np.abs(spec[:2 * N, 0] - mag_ref)) <= 1e-5 * np.max(mag_ref)
     big = mag_ref > 1e-3 * mag_ref.max()
     assert np.max(np.abs(spec[:2 * N, 1][big] - ref.imag[big])) < 1e-3
+
+
+def test_table_blob_roundtrip_and_validation(cuda):
+    """The init-time broadcast payload: export -> import into another
+    handle of the same configuration keeps outputs bit-identical; a blob built for a
+    different configuration is rejected."""
+    import torch
+    from pvamd import PVError
+    x = synth(20000, 9)
+    a = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=100)
+    b = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=100)
+    blob = a.export_tables()
+    assert blob.numel() > 1024 * 4
+    b.import_tables(blob)
+    assert torch.equal(b.export_tables(), blob)
+    oa, _ = a.process(to_dev(x))
+    ob, _ = b.process(to_dev(x))
+    assert torch.equal(oa, ob)
+    c = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=100)
+    with pytest.raises(PVError):
+        c.import_tables(blob)
+
+
+def test_edge_cases_empty_short_and_silence(cuda):
+    import torch
+    pv = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=100)
+    # n <= hop: no frames (main.cpp:231 loop never runs)
+    assert pv.num_frames(200) == 0
+    out, spec = pv.process(torch.zeros(200, device="cuda"))
+    assert out.numel() == 0 and spec.numel() == 0
+    # n < N: frames read zeros past the end
+    x = synth(700, 4)
+    out, _ = pv.process(to_dev(x))
+    ref = pvref.std_process(x, 1024, 4, ord("t"), 0.5)
+    assert out.shape[1] == ref.shape[0] and rms(out.cpu().numpy()[0], ref) <= RMS_TOL
+    # digital silence then signal (autotune.wav starts with 1124 zeros): zero bins have
+    # phase 0 by definition, so the unwrap state stays in step with the oracle
+    x = np.concatenate([np.zeros(5000, np.float32), synth(20000, 5)])
+    out, spec = pv.process(to_dev(x))
+    ref = pvref.std_process(x, 1024, 4, ord("t"), 0.5)
+    assert rms(out.cpu().numpy()[0], ref) <= RMS_TOL
+    assert torch.all(spec[0, 0, :513, 1] == 0)
+
+
+def test_ragged_channel_strides_and_determinism(cuda):
+    """channels with a row stride larger than n; two runs must be bit-identical."""
+    import torch
+    C, n, ld = 3, 15000, 16384
+    xs = np.zeros((C, ld), np.float32)
+    for c in range(C):
+        xs[c, :n] = synth(n, 100 + c)
+    dev = to_dev(xs)
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 1.5, 4, mode=STANDARD, max_channels=C, max_frames=100)
+    o1, _ = pv.process(dev, n_samples=n)
+    o2, _ = pv.process(dev, n_samples=n)
+    assert torch.equal(o1, o2)
+    for c in range(C):
+        ref = pvref.std_process(xs[c, :n], 1024, 4, ord("p"), 1.5)
+        assert rms(o1[c].cpu().numpy(), ref) <= RMS_TOL
