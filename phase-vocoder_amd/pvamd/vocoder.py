@@ -195,7 +195,7 @@ class PhaseVocoder:
         torch = _torch()
         n = ctypes.c_size_t()
         self._call(self._L.pv_export_tables(self._h, None, 0, ctypes.byref(n), None), "pv_export_tables")
-        blob = torch.empty(n.value, dtype=torch.uint8, device=f"cuda:{self.device}")
+        blob = torch.zeros(n.value, dtype=torch.uint8, device=f"cuda:{self.device}")
         self._call(self._L.pv_export_tables(self._h, _ptr(blob), n.value, ctypes.byref(n),
                                             self._stream()), "pv_export_tables")
         return blob
