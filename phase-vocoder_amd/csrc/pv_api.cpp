@@ -253,9 +253,11 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.out = out;
     p.ldo = ldo;
     p.out_len = olen;
+    p.out_aligned = ((reinterpret_cast<uintptr_t>(out) & 7) == 0) && ((ldo & 1) == 0);
     p.tails = h->d_tails;
     p.tail_len = h->tail_len;
-    PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, h->mode == PV_MODE_STANDARD ? 0 : 1, C, p, s));
+    const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
+    PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, smode, C, p, s));
     const int nwg = (nruns + 3) / 4;
     if (nwg > 1 || ola_in != nullptr) {
         pv::SeamParams sm{};
@@ -496,7 +498,7 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
 
     // LDS budget check for the synthesis kernel (largest)
-    size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->bins_pad, 0);
+    size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->hs);
     if (lds > 160 * 1024) return bail(fail(PV_ERR_UNSUPPORTED, "LDS budget exceeded"));
     *out = h;
     return PV_OK;

@@ -92,12 +92,12 @@ __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) 
 }
 
 // ------------------------------------------------------------------ wave-local LDS sync
-// A frame's LDS tile is private to one wave; LDS executes a wave's DS instructions in
-// order, so a compiler fence + wave barrier orders the cross-lane exchange.
+// A frame's LDS tile is private to one wave and the LDS executes one wave's DS
+// instructions in issue order, so a cross-lane exchange (ds_write by lane a, later
+// ds_read by lane b) needs no s_waitcnt: only the compiler must keep program order,
+// which the memory clobber enforces.
 __device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 // ------------------------------------------------------------------ FFT geometry
@@ -112,6 +112,9 @@ struct Geo {
     static constexpr int TILE = L + (L >> PADSH) + 2;  // padded LDS tile (float2), +bin L
     static_assert(L >= 128 && L <= 2048, "one frame per wave: L in [128, 2048]");
     __device__ static __forceinline__ int pad(int p) { return p + (p >> PADSH); }
+    // pad(a + c) = pad(a) + padc(c) whenever c or a is a multiple of E (all access
+    // patterns below): one per-lane base address plus a compile-time offset.
+    static constexpr int padc(int c) { return c + (c >> PADSH); }
 };
 
 // Stage-major twiddle table: stage Ns occupies [Ns-1, 2Ns-1), entry idx = e^{-i pi idx/Ns}
@@ -121,7 +124,8 @@ struct Geo {
 // Input layout : v[g*R + q] = x[j + q*L/R],   j = lane + 64 g
 // Output layout: v[g*R + f] = y[(j/S)*R*S + j%S + S*bitrev_r(f)]
 template <int L, int P, bool INV>
-__device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* tw, int lane) {
+__device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* tw,
+                                         const float2 (&tw0)[Geo<L>::E], int lane) {
     using G_ = Geo<L>;
     constexpr int S = 1 << (P * G_::RLOG);
     constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
@@ -141,7 +145,8 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
 #pragma unroll
             for (int s = 0; s < R / 2; ++s) {
                 const int br = bitrevc(s & ((1 << st) - 1), st);
-                float2 w = tw[(Ns - 1) + jm + S * br];
+                // pass 0: jm = 0, S = 1: compile-time index into the hoisted tw0 (SGPRs)
+                float2 w = (P == 0) ? tw0[(Ns - 1) + br] : tw[(Ns - 1) + jm + S * br];
                 if (INV) w.y = -w.y;
                 const float2 top = a[s];
                 const float2 t = cmul(a[s + R / 2], w);
@@ -169,8 +174,9 @@ __device__ __forceinline__ void pass_store(const float2 (&v)[Geo<L>::E], float2*
     for (int g = 0; g < NG; ++g) {
         const int j = lane + 64 * g;
         const int J = (j / S) * R * S + (j & (S - 1));
+        float2* base = tile + G_::pad(J);  // J = 0 mod E when S = 1; S*br = 0 mod E when S >= E
 #pragma unroll
-        for (int f = 0; f < R; ++f) tile[G_::pad(J + S * bitrevc(f, r))] = v[g * R + f];
+        for (int f = 0; f < R; ++f) base[G_::padc(S * bitrevc(f, r))] = v[g * R + f];
     }
 }
 
@@ -180,27 +186,53 @@ __device__ __forceinline__ void pass_load(float2 (&v)[Geo<L>::E], const float2* 
     constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
     constexpr int R = 1 << r;
     constexpr int NG = G_::E / R;
+    const float2* base = tile + G_::pad(lane);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-        const int j = lane + 64 * g;
 #pragma unroll
-        for (int q = 0; q < R; ++q) v[g * R + q] = tile[G_::pad(j + q * (L / R))];
+        for (int q = 0; q < R; ++q) v[g * R + q] = base[G_::padc(64 * g + q * (L / R))];
     }
 }
 
-// Full FFT: v holds the pass-0 input layout (x[lane + 64 q], since R0 = E); the result is
-// left in `tile` in natural order (padded indexing).
-template <int L, bool INV, int P = 0>
+// Pass-0 twiddles (stage-major entries 0..E-2): wave-uniform, loaded once per kernel from
+// global memory so they live in SGPRs (s_load) instead of costing LDS reads every frame.
+template <int L>
+__device__ __forceinline__ void load_tw0(float2 (&tw0)[Geo<L>::E], const float2* __restrict__ tw) {
+#pragma unroll
+    for (int i = 0; i + 1 < Geo<L>::E; ++i) tw0[i] = tw[i];
+    tw0[Geo<L>::E - 1] = make_float2(1.0f, 0.0f);
+}
+
+// Full FFT: v holds the pass-0 input layout (x[lane + 64 q], since R0 = E).  With
+// STORE_LAST the result is left in `tile` in natural order (padded indexing); without it
+// the last pass's output stays in v, where register v[g*R + f] holds point
+// lane + 64 g + S_last * bitrev_r(f)  (= lane + 64 c, see last_slot()).
+template <int L, bool INV, bool STORE_LAST = true, int P = 0>
 __device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, const float2* tw,
-                                        int lane) {
-    fft_pass<L, P, INV>(v, tw, lane);
-    pass_store<L, P>(v, tile, lane);
-    wave_lds_sync();
+                                        const float2 (&tw0)[Geo<L>::E], int lane) {
+    fft_pass<L, P, INV>(v, tw, tw0, lane);
     if constexpr (P + 1 < Geo<L>::NPASS) {
+        pass_store<L, P>(v, tile, lane);
+        wave_lds_sync();
         pass_load<L, P + 1>(v, tile, lane);
         wave_lds_sync();
-        fft_run<L, INV, P + 1>(v, tile, tw, lane);
+        fft_run<L, INV, STORE_LAST, P + 1>(v, tile, tw, tw0, lane);
+    } else if constexpr (STORE_LAST) {
+        pass_store<L, P>(v, tile, lane);
+        wave_lds_sync();
     }
+}
+
+// slot c of register idx after the last pass: point = lane + 64 * last_slot(idx)
+template <int L>
+constexpr int last_slot(int idx) {
+    using G_ = Geo<L>;
+    constexpr int P = G_::NPASS - 1;
+    constexpr int S = 1 << (P * G_::RLOG);
+    constexpr int r = G_::LOG2L - P * G_::RLOG;
+    constexpr int R = 1 << r;
+    const int g = idx / R, f = idx % R;
+    return g + (S / 64) * bitrevc(f, r);
 }
 
 }  // namespace pv

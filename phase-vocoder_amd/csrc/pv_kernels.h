@@ -52,6 +52,7 @@ struct SynParams {
     int hs;                            // out hop
     float* out;
     long long ldo, out_len;
+    int out_aligned;                   // out base and ldo allow 8-byte vector stores
     float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
     int tail_len;
 };
@@ -71,7 +72,7 @@ hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
-size_t synthesis_lds_bytes(int L, int bins_pad, int ring);
+size_t synthesis_lds_bytes(int L, int hs);
 hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,
                                int n, int hop, hipStream_t s);
 

@@ -93,6 +93,45 @@ __device__ __forceinline__ void real_split_all(const float2* tile, const float2*
     }
 }
 
+// Bins i0 .. i0+CH-1 of a lane (reads batched; entries past E are dummies).
+template <int L, int CH>
+__device__ __forceinline__ void split_chunk(const float2* tile, const float2* twsl, int lane, int i0,
+                                            float2 (&X)[CH]) {
+    using G_ = Geo<L>;
+    constexpr int E = G_::E;
+    // A = Z[k], B = Z[(L-k) mod L], k = lane + 64 i: affine in i from two per-lane bases;
+    // only (lane 0, i = 0) wraps (B = Z[0]) and bin L (i = E, lane 0) uses Z[0] twice.
+    const float2* baseA = tile + G_::pad(lane);
+    const float2* baseB = tile + G_::pad(L - lane);
+    const float2* baseT = twsl + lane;
+    float2 A[CH], Bz[CH], tw[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        if (i < E) {
+            A[c] = baseA[G_::padc(64 * i)];
+            Bz[c] = (i == 0 && lane == 0) ? tile[0] : baseB[-G_::padc(64 * i)];
+            tw[c] = baseT[64 * i];
+        } else {
+            A[c] = tile[0];
+            Bz[c] = tile[0];
+            tw[c] = twsl[L];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        const float er = 0.5f * (A[c].x + Bz[c].x);
+        const float ei = 0.5f * (A[c].y - Bz[c].y);
+        const float orr = 0.5f * (A[c].y + Bz[c].y);
+        const float oi = 0.5f * (Bz[c].x - A[c].x);
+        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
+        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
+        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
+        X[c] = make_float2(Xr, Xi);
+    }
+}
+
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
 #define PV_FOR_BINS(E_, lane_, ...)                              \
     _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \
@@ -107,7 +146,7 @@ __device__ __forceinline__ void real_split_all(const float2* tile, const float2*
 // for its phase).  The unwrap decision m(t) = f(phi[t], phi[t-1]) is accumulated in
 // registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
 template <int L>
-__global__ __launch_bounds__(256) void k_std_analysis(AnaParams p) {
+__global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -121,6 +160,8 @@ __global__ __launch_bounds__(256) void k_std_analysis(AnaParams p) {
     const int BP = p.bins_pad;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float2 tw0[Geo<L>::E];
+    load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
     for (int i = tid; i < B; i += 256) { twsl[i] = p.tws[i]; ekl[i] = p.ek[i]; }
     for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
@@ -137,26 +178,8 @@ __global__ __launch_bounds__(256) void k_std_analysis(AnaParams p) {
     int sacc[E + 1], m0[E + 1];
     PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; m0[i] = 0; })
 
-    // raw samples of the next frame are loaded one frame ahead (software pipeline)
-    auto fetch = [&](int t, float2 (&xr)[E]) {
-        const long long base = (long long)t * p.hop;
-        if (p.aligned && base + N <= p.n) {
-#pragma unroll
-            for (int q = 0; q < E; ++q)
-                xr[q] = *reinterpret_cast<const float2*>(xc + base + 2 * (lane + 64 * q));
-        } else {
-#pragma unroll
-            for (int q = 0; q < E; ++q) {
-                const long long s = base + 2 * (lane + 64 * q);
-                xr[q].x = (s < p.n) ? xc[s] : 0.0f;
-                xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
-            }
-        }
-    };
-    const int u0 = (t0 > 0) ? -1 : 0;
-    float2 xr[E];
-    fetch(t0 + u0, xr);
-    for (int u = u0; u < nfr; ++u) {
+    // One frame: window + FFT + split + atan2 (+ spectrum row, decisions) from raw samples.
+    auto frame = [&](int u, const float2 (&xr)[E]) {
         const int t = t0 + u;
         float2 z[E];
 #pragma unroll
@@ -165,24 +188,70 @@ __global__ __launch_bounds__(256) void k_std_analysis(AnaParams p) {
             z[q].x = xr[q].x * wv.x;
             z[q].y = xr[q].y * wv.y;
         }
-        if (u + 1 < nfr) fetch(t + 1, xr);
-        fft_run<L, false>(z, tile, twl, lane);
-        float2 X[E + 1];
-        real_split_all<L>(tile, twsl, lane, X);
-        wave_lds_sync();  // tile reads done before the next frame's pass_store
-        float ph[E + 1];
-        PV_FOR_BINS(E, lane, { ph[i] = atan2_pv(X[i].y, X[i].x); })
-        if (u >= 0) {
-            float2* srow = specc + (long long)t * p.spec_stride;
-            PV_FOR_BINS(E, lane, {
-                const float mag = __builtin_sqrtf(__builtin_fmaf(X[i].x, X[i].x, X[i].y * X[i].y));
-                srow[k] = make_float2(mag, ph[i]);
-                const int m = unwrap_count(ph[i], phprev[i], ekl[k]);
-                m0[i] = (u == 0) ? m : m0[i];
-                sacc[i] += (u == 0) ? 0 : m;
-            })
+        fft_run<L, false>(z, tile, twl, tw0, lane);
+        // bins in chunks of CH (bounded live registers), all reads of a chunk batched
+        constexpr int CH = 3;
+        float2* srow = specc + (long long)t * p.spec_stride;
+#pragma unroll
+        for (int i0 = 0; i0 <= E; i0 += CH) {
+            float2 X[CH];
+            split_chunk<L, CH>(tile, twsl, lane, i0, X);
+#pragma unroll
+            for (int c2 = 0; c2 < CH; ++c2) {
+                const int i = i0 + c2;
+                if (i > E || (i == E && lane != 0)) break;
+                const int k = (i == E) ? L : lane + 64 * i;
+                const float ph = atan2_pv(X[c2].y, X[c2].x);
+                if (u >= 0) {
+                    const float mag = __builtin_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    srow[k] = make_float2(mag, ph);
+                    const int m = unwrap_count(ph, phprev[i], ekl[k]);
+                    if (u == 0) m0[i] = m;
+                    sacc[i] += (u == 0) ? 0 : m;
+                }
+                phprev[i] = ph;
+            }
         }
-        PV_FOR_BINS(E, lane, { phprev[i] = ph[i]; })
+        wave_lds_sync();  // tile reads done before the next frame's pass_store
+    };
+    const int u0 = (t0 > 0) ? -1 : 0;
+    // frames whose N samples are all inside [0, n) take the vector-load path with the raw
+    // samples fetched one frame ahead; the (at most N/hop) frames at the end of a channel
+    // take the bounds-checked path.
+    int ufast = u0;
+    if (p.aligned) {
+        const long long lastfull = (p.n - N) / p.hop;  // last frame index fully inside
+        ufast = (int)min((long long)nfr, max((long long)u0, lastfull - t0 + 1));
+    }
+    {
+        float2 xr[E];
+        if (u0 < ufast) {
+            const float* src = xc + (long long)(t0 + u0) * p.hop;
+#pragma unroll
+            for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
+        }
+        for (int u = u0; u < ufast; ++u) {
+            float2 cur[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) cur[q] = xr[q];
+            if (u + 1 < ufast) {
+                const float* src = xc + (long long)(t0 + u + 1) * p.hop;
+#pragma unroll
+                for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
+            }
+            frame(u, cur);
+        }
+    }
+    for (int u = ufast; u < nfr; ++u) {
+        float2 xr[E];
+        const long long base = (long long)(t0 + u) * p.hop;
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const long long s = base + 2 * (lane + 64 * q);
+            xr[q].x = (s < p.n) ? xc[s] : 0.0f;
+            xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
+        }
+        frame(u, xr);
     }
     if (p.runsum != nullptr) {
         int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * BP;
@@ -204,6 +273,8 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     float2* tiles = twl + L;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float2 tw0[Geo<L>::E];
+    load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
     __syncthreads();
     const int run = blockIdx.x * 4 + w, c = blockIdx.y;
@@ -235,7 +306,7 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
             }
             z[q] = make_float2(b0, b1);
         }
-        fft_run<L, false>(z, tile, twl, lane);
+        fft_run<L, false>(z, tile, twl, tw0, lane);
         float2* srow = specc + (long long)t * p.spec_stride;
         PV_FOR_BINS(E, lane, {
             const float2 X = real_split<L>(tile, p.tws, k);
@@ -308,16 +379,22 @@ __global__ __launch_bounds__(256) void k_carry(ScanParams p) {
 
 // ------------------------------------------------------------------ K3 synthesis
 // One wave = one run of F frames (virtually padded to F: frames >= `frames` are zero).
-// MODE 0: STANDARD — output phase rho*(phi + 2 pi (M_dec + (t+1) j_k)),
+// MODE 0/2: STANDARD time stretch / pitch shift — output phase rho*(phi + 2 pi (M_dec + (t+1) j_k)),
 //         Hann synthesis window with overlap normalisation folded into gain[].
 // MODE 1: REF_COMPAT — kernel.cu:352-432: x' = m cos(phi), y' = x' sin(phi), C2R N, /N,
 //         swap halves (rot = N/2), Hamming window (gain = w/N).
-// Overlap-add: per-wave LDS ring of N samples; a position is final once the frame that
-// starts after it has been added; final samples are stored straight to `out`.  After the
-// loop the three intra-workgroup seams are closed from the neighbours' rings (one
-// barrier); the workgroup's last tail goes to `tails` for k_seam.
-template <int L, int MODE>
-__global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
+// Overlap-add: a position is final once the frame that starts after it has been added;
+// final samples are stored straight to `out`.
+//   ROLA (out hop a multiple of 128, L <= 1024): in registers.  After the inverse FFT's last
+//     pass lane holds points lane + 64 c, i.e. samples 2 lane + {0,1} + 128 c, so every
+//     position a lane ever touches is congruent to 2 lane (+1) mod 128: the accumulator
+//     acc[c] covers run positions u*hs + 128 c + 2 lane + {0,1}; per frame the oldest
+//     hs/128 slots are stored and the rest shift down.  No LDS ring, no final FFT store.
+//   otherwise: per-wave LDS ring of N samples.
+// After the loop the three intra-workgroup seams are closed from the neighbours' tails in
+// LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
+template <int L, int MODE, bool ROLA>
+__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -328,26 +405,32 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
     float2* twsl = twl + L;                                            // L (+2 pad)
     float2* tiles = twsl + (L + 2);                                    // 4 x TILE
     float* rings = reinterpret_cast<float*>(tiles + 4 * G_::TILE);    // 4 x N
-    float* gainl = rings + 4 * N;                                      // N
-    float* ekl = gainl + N;                                            // B (+pad)
+    float* gainl = rings + 4 * N;                                      // N (ring path)
+    float* ekl = gainl + ((ROLA && L <= 512) ? 0 : N);                 // B (+pad)
     unsigned* jkl = reinterpret_cast<unsigned*>(ekl + (B + 3));        // B (+pad)
     int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
     const int hs = p.hs;
     const int TL = N - hs;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float2 tw0[Geo<L>::E];
+    load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) { twl[i] = p.tw[i]; twsl[i] = p.tws[i]; }
-    for (int i = tid; i < N; i += 256) gainl[i] = p.gain[i];
-    if (MODE == 0) {
+    constexpr bool GREG = ROLA && L <= 512;  // ROLA gains in registers (else LDS float2 reads)
+    if (!GREG)
+        for (int i = tid; i < N; i += 256) gainl[i] = p.gain[i];
+    if (MODE != 1) {
         for (int i = tid; i < B; i += 256) {
             ekl[i] = p.ek[i];
             jkl[i] = p.jk_mod[i];
-            if (p.pitch) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
+            if (MODE == 2) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
         }
     }
-    float* ring = rings + w * N;
+    float* ring = rings + w * N;  // ROLA: the run's tail, written after the frame loop
+    if (!ROLA) {
 #pragma unroll
-    for (int i = 0; i < SPW; ++i) ring[lane + 64 * i] = 0.0f;
+        for (int i = 0; i < SPW; ++i) ring[lane + 64 * i] = 0.0f;
+    }
     __syncthreads();
 
     const int c = blockIdx.y;
@@ -361,9 +444,22 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
 
     int M[E + 1];
     float phprev[E + 1];
-    if (MODE == 0 && nfr > 0) {
+    if (MODE != 1 && nfr > 0) {
         const int* cr = p.carry + ((long long)c * p.nruns + run) * p.bins_pad;
         PV_FOR_BINS(E, lane, { M[i] = cr[k]; phprev[i] = 0.0f; })
+    }
+
+    // ROLA state: acc[c] = run positions u*hs + 128 c + 2 lane + {0,1}; gains likewise
+    constexpr int NS = ROLA ? E : 1;
+    float2 acc[NS], gn[GREG ? NS : 1];
+    const int D = hs >> 7;  // slots completed per frame (ROLA)
+    if (ROLA) {
+        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            acc[s] = make_float2(0.0f, 0.0f);
+            if constexpr (GREG) gn[s] = g2[64 * s + lane];
+        }
     }
 
     float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
@@ -380,7 +476,7 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
                 const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
                 PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
             }
-            if (MODE == 0) {
+            if (MODE != 1) {
                 const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
                 float phc[E + 1];
                 float ekv[E + 1];
@@ -407,7 +503,7 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
                         phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x % qq) * p.inv_q));
                     })
                 }
-                if (p.pitch) {
+                if constexpr (MODE == 2) {
                     float2 Y[E + 1];
                     PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
                     wave_lds_sync();
@@ -451,11 +547,13 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
             wave_lds_sync();
             // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
             float2 z[E];
+            const float2* baseA = tile + G_::pad(lane);
+            const float2* baseB = tile + G_::pad(L - lane);
 #pragma unroll
             for (int q = 0; q < E; ++q) {
                 const int i = lane + 64 * q;
-                const float2 A = tile[G_::pad(i)];
-                const float2 Bc = tile[G_::pad(L - i)];
+                const float2 A = baseA[G_::padc(64 * q)];
+                const float2 Bc = baseB[-G_::padc(64 * q)];
                 const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
                 const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
                 const float2 tw = twsl[i];                       // e^{-2 pi i k/N}
@@ -464,28 +562,72 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
                 z[q] = make_float2(fer - Foi, fei + For);
             }
             wave_lds_sync();
-            fft_run<L, true>(z, tile, twl, lane);
-            // overlap-add the frame into the ring (lane-distinct positions)
-            const float* ty = reinterpret_cast<const float*>(tile);
+            if constexpr (ROLA) {
+                fft_run<L, true, false>(z, tile, twl, tw0, lane);
+                // register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
+                // moves raw slot cr to OLA slot cr + E/2 (mod E)
 #pragma unroll
-            for (int i = 0; i < SPW; ++i) {
-                const int n = lane + 64 * i;
-                const int nn = (n + p.rot) & (N - 1);
-                const float yv = ty[2 * G_::pad(nn >> 1) + (nn & 1)];
-                const int pos = (u * hs + n) & (N - 1);
-                ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
+                for (int idx = 0; idx < E; ++idx) {
+                    const int cr = last_slot<L>(idx);
+                    const int cs = (MODE == 1) ? ((cr + E / 2) & (E - 1)) : cr;
+                    const float2 g = GREG ? gn[GREG ? cs : 0]
+                                          : reinterpret_cast<const float2*>(gainl)[64 * cs + lane];
+                    acc[cs].x = __builtin_fmaf(z[idx].x, g.x, acc[cs].x);
+                    acc[cs].y = __builtin_fmaf(z[idx].y, g.y, acc[cs].y);
+                }
+            } else {
+                fft_run<L, true>(z, tile, twl, tw0, lane);
+                // overlap-add the frame into the ring (lane-distinct positions)
+                // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
+                // 2 pad(nn >> 1) + (nn & 1) = per-lane base + compile-time offset
+                constexpr int ROT = (MODE == 1) ? N / 2 : 0;
+                const float* ty = reinterpret_cast<const float*>(tile) + 2 * G_::pad(lane >> 1) + (lane & 1);
+                const int rbase = u * hs + lane;
+#pragma unroll
+                for (int i = 0; i < SPW; ++i) {
+                    const int n = lane + 64 * i;
+                    const int c = ((64 * i + ROT) & (N - 1)) >> 1;
+                    const float yv = ty[2 * G_::padc(c)];
+                    const int pos = (rbase + 64 * i) & (N - 1);
+                    ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
+                }
+                wave_lds_sync();
+            }
+        }
+        if constexpr (ROLA) {
+            // positions [u*hs, (u+1)*hs) = slots 0..D-1 are final: store, shift down
+            const long long pb = obase + (long long)u * hs + 2 * lane;
+            for (int d = 0; d < D; ++d) {
+                const long long gp = pb + 128 * d;
+                if (p.out_aligned && gp + 1 < p.out_len) {
+                    *reinterpret_cast<float2*>(outc + gp) = acc[0];
+                } else {
+                    if (gp < p.out_len) outc[gp] = acc[0].x;
+                    if (gp + 1 < p.out_len) outc[gp + 1] = acc[0].y;
+                }
+#pragma unroll
+                for (int s = 0; s + 1 < NS; ++s) acc[s] = acc[s + 1];
+                acc[NS - 1] = make_float2(0.0f, 0.0f);
+            }
+        } else {
+            // positions [u*hs, (u+1)*hs) are final for this run
+            for (int j = lane; j < hs; j += 64) {
+                const int pl = u * hs + j;
+                const int slot = pl & (N - 1);
+                const float v = ring[slot];
+                ring[slot] = 0.0f;
+                if (obase + pl < p.out_len) outc[obase + pl] = v;
             }
             wave_lds_sync();
         }
-        // positions [u*hs, (u+1)*hs) are final for this run
-        for (int j = lane; j < hs; j += 64) {
-            const int pl = u * hs + j;
-            const int slot = pl & (N - 1);
-            const float v = ring[slot];
-            ring[slot] = 0.0f;
-            if (obase + pl < p.out_len) outc[obase + pl] = v;
-        }
-        wave_lds_sync();
+    }
+    if constexpr (ROLA) {
+        // the run's tail (positions F*hs + j, j < N - hs) -> ring[j]; ring index of tail
+        // position j below is then (F*hs + j) & (N-1) rewritten as j via tail_at()
+        float2* r2 = reinterpret_cast<float2*>(ring);
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            if (s < NS - D) r2[64 * s + lane] = acc[s];
     }
     __syncthreads();
     // seams: run w's tail (ring positions [F*hs, F*hs + TL)) overlaps run w+1's head
@@ -493,7 +635,7 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
         const float* prev = rings + (w - 1) * N;
         for (int j = lane; j < TL; j += 64) {
             const long long gp = obase + j;
-            if (gp < p.out_len) outc[gp] += prev[(p.F * hs + j) & (N - 1)];
+            if (gp < p.out_len) outc[gp] += prev[ROLA ? j : ((p.F * hs + j) & (N - 1))];
         }
     }
     if (w == 3) {
@@ -501,7 +643,7 @@ __global__ __launch_bounds__(256) void k_synthesis(SynParams p) {
         const bool last = (blockIdx.x + 1 >= nwg);
         float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len;
         for (int j = lane; j < TL; j += 64) {
-            const float v = ring[(p.F * hs + j) & (N - 1)];
+            const float v = ring[ROLA ? j : ((p.F * hs + j) & (N - 1))];
             if (last) {
                 const long long gp = obase + (long long)p.F * hs + j;
                 if (gp < p.out_len) outc[gp] = v;
@@ -558,19 +700,25 @@ template <int L>
 static size_t ana_lds_compat() {
     return sizeof(float2) * (L + 4 * Geo<L>::TILE);
 }
+// twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with ROLA at L <= 512
+// the gains live in registers and gainl is not allocated (it is the last float array before ekl,
+// so ekl/jkl/srcl simply start N floats earlier: see the kernel's carve-up)
 template <int L>
-static size_t syn_lds(int, int) {
-    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * 5 * (2 * L) +
-           sizeof(float) * 4 * (L + 1 + 3);
+static size_t syn_lds(bool rola) {
+    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) +
+           sizeof(float) * ((rola && L <= 512) ? 4 : 5) * (2 * L) + sizeof(float) * 4 * (L + 1 + 3);
 }
 
-size_t synthesis_lds_bytes(int L, int bins_pad, int ring) {
+static bool syn_rola(int L, int hs) { return (hs % 128 == 0) && L <= 1024; }
+
+size_t synthesis_lds_bytes(int L, int hs) {
+    const bool r = syn_rola(L, hs);
     switch (L) {
-        case 128: return syn_lds<128>(bins_pad, ring);
-        case 256: return syn_lds<256>(bins_pad, ring);
-        case 512: return syn_lds<512>(bins_pad, ring);
-        case 1024: return syn_lds<1024>(bins_pad, ring);
-        case 2048: return syn_lds<2048>(bins_pad, ring);
+        case 128: return syn_lds<128>(r);
+        case 256: return syn_lds<256>(r);
+        case 512: return syn_lds<512>(r);
+        case 1024: return syn_lds<1024>(r);
+        case 2048: return syn_lds<2048>(r);
     }
     return 0;
 }
@@ -615,17 +763,21 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
 
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
+    const bool rola = syn_rola(L, p.hs);
+#define PV_SYN(M_, R_)                                                                   \
+    PV_DISPATCH_L(L, {                                                                   \
+        hipLaunchKernelGGL((k_synthesis<LL, M_, R_ && (LL <= 1024)>), grid, dim3(256),   \
+                           syn_lds<LL>(R_ && (LL <= 1024)), s, p);                      \
+    })
+    // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
     if (mode == 0) {
-        PV_DISPATCH_L(L, {
-            hipLaunchKernelGGL((k_synthesis<LL, 0>), grid, dim3(256),
-                               syn_lds<LL>(0, 0), s, p);
-        });
+        if (rola) { PV_SYN(0, true); } else { PV_SYN(0, false); }
+    } else if (mode == 2) {
+        if (rola) { PV_SYN(2, true); } else { PV_SYN(2, false); }
     } else {
-        PV_DISPATCH_L(L, {
-            hipLaunchKernelGGL((k_synthesis<LL, 1>), grid, dim3(256),
-                               syn_lds<LL>(0, 0), s, p);
-        });
+        if (rola) { PV_SYN(1, true); } else { PV_SYN(1, false); }
     }
+#undef PV_SYN
     return hipGetLastError();
 }
 

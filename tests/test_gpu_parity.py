@@ -163,3 +163,44 @@ def test_ragged_channel_strides_and_determinism(cuda):
     for c in range(C):
         ref = pvref.std_process(xs[c, :n], 1024, 4, ord("p"), 1.5)
         assert rms(o1[c].cpu().numpy(), ref) <= RMS_TOL
+
+
+@pytest.mark.parametrize("N,hop_div,effect,scale", [
+    (256, 2, TIME_SHIFT, 1.0),     # L=128, out hop 128: register overlap-add
+    (512, 4, TIME_SHIFT, 1.0),     # L=256, out hop 128
+    (512, 4, PITCH_SHIFT, 1.25),   # L=256, out hop 128, pitch map
+    (2048, 4, TIME_SHIFT, 1.0),    # L=1024, out hop 512
+    (2048, 4, PITCH_SHIFT, 0.8),   # L=1024, pitch
+    (256, 4, TIME_SHIFT, 1.0),     # out hop 64: LDS ring overlap-add
+    (1024, 4, TIME_SHIFT, 0.75),   # out hop 192: LDS ring overlap-add
+    (2048, 8, TIME_SHIFT, 1.0),    # L=1024, out hop 256
+])
+def test_std_process_parity_geometries(cuda, N, hop_div, effect, scale):
+    """Both overlap-add paths (registers when the out hop is a multiple of 128 and
+    L <= 1024, LDS ring otherwise) across FFT sizes."""
+    x = synth(40000, 31)
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_frames=2000)
+    out, _ = pv.process(to_dev(x))
+    ref = pvref.std_process(x, N, hop_div, ord(effect), scale)
+    assert out.shape[1] == ref.shape[0]
+    assert rms(out.cpu().numpy()[0], ref) <= RMS_TOL
+
+
+@pytest.mark.parametrize("mode", [STANDARD, REF_COMPAT])
+def test_odd_output_stride(cuda, mode):
+    """out rows at an odd float stride: the vectorised stores must fall back to scalar."""
+    import torch
+    C, N = 3, 1024
+    xs = np.stack([synth(25000, 60 + c) for c in range(C)])
+    pv = PhaseVocoder(N, TIME_SHIFT, 0.5 if mode == STANDARD else 1.0, 4, mode=mode,
+                      max_channels=C, max_frames=200)
+    frames = pv.num_frames(xs.shape[1])
+    olen = pv.output_length(frames)
+    big = torch.full((C, olen + 1 if olen % 2 == 0 else olen + 2), 7.0, device="cuda")
+    out = big[:, :olen]
+    assert out.stride(0) % 2 == 1
+    spec = pv.alloc_spec(C, frames)
+    pv.process(to_dev(xs), spec=spec, out=out)
+    dense, _ = pv.process(to_dev(xs))
+    assert torch.equal(out, dense)
+    assert torch.all(big[:, olen:] == 7.0)  # nothing written past the row
