@@ -28,6 +28,84 @@ constexpr float kPi = 0x1.921fb6p+1f;
 constexpr float kTwoPi = 0x1.921fb6p+2f;
 constexpr float kInv2Pi = 0x1.45f306p-3f;
 
+// native 2-vector: arithmetic on it selects the packed fp32 VALU ops (v_pk_mul/add/fma_f32)
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// cmul() with packed ops, two VOP3P instructions whose modifiers do the swizzles:
+//   p = (b.y * -w.y, b.y * w.x)     v_pk_mul_f32 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]
+//   t = (fma(b.x, w.x, p.x), fma(b.x, w.y, p.y))   v_pk_fma_f32 op_sel_hi:[0,1,1]
+// (-(b.y w.y) = b.y (-w.y) exactly), i.e. the same roundings as cmul().  CONJ uses
+// conj(w) = (w.x, -w.y) through the neg modifiers instead of a register copy.
+// Plain C++ vector code makes the compiler materialise the negated / swapped twiddle
+// with extra moves, hence the asm.  WS: the twiddle lives in SGPRs (pass 0, tw0).
+template <bool CONJ, bool WS = false>
+__device__ __forceinline__ f2v cmul_v(f2v b, f2v w) {
+    f2v p, t;
+    if constexpr (!CONJ) {
+        if constexpr (WS) {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(p) : "v"(b), "s"(w));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(b), "s"(w), "v"(p));
+        } else {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(p) : "v"(b), "v"(w));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(b), "v"(w), "v"(p));
+        }
+    } else {
+        // w' = (w.x, -w.y): p = (b.y w.y, b.y w.x), t = (fma(b.x, w.x, p.x), fma(b.x, -w.y, p.y))
+        if constexpr (WS) {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(p) : "v"(b), "s"(w));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(t) : "v"(b), "s"(w), "v"(p));
+        } else {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(p) : "v"(b), "v"(w));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(t) : "v"(b), "v"(w), "v"(p));
+        }
+    }
+    return t;
+}
+
+// LDS loads the compiler must not pair into ds_read2_b32/_b64: a paired read costs 4x the
+// LDS cycles of the same bytes as ds_read_b64 (MI355X_MICROARCH.md §LDS).  Volatile
+// accesses are never merged; they still schedule freely against non-volatile code.
+#define PV_LDS __attribute__((address_space(3)))
+__device__ __forceinline__ float2 lds_ld(const float2* p) {
+    const f2v v = *(const volatile PV_LDS f2v*)(p);  // explicit LDS: volatile blocks the
+    return make_float2(v.x, v.y);                      // generic->LDS address-space inference
+}
+__device__ __forceinline__ float lds_ld(const float* p) { return *(const volatile PV_LDS float*)(p); }
+__device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return *(const volatile PV_LDS unsigned*)(p); }
+__device__ __forceinline__ int lds_ld(const int* p) { return *(const volatile PV_LDS int*)(p); }
+
+// ---------------------------------------------------------------------------
+// Self-tracked prefetch.  vmcnt counts loads and stores together in issue order and the
+// compiler's wait insertion merges paths conservatively, which in a frame loop turns
+// "wait for the prefetched samples" into "drain the previous frame's stores too".  These
+// loads are invisible to the compiler's wait insertion; the caller issues them, then
+// exactly K unconditional stores, then vm_wait<K>, all within one loop trip (so the
+// registers are never copied or spilled while the loads are in flight; check
+// "VGPRs Spill: 0" in the resource-usage report).
+template <int E>
+__device__ __forceinline__ void gload_pairs(f2v (&xr)[E], const float* src) {
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        const float* pq = src + 1024 * (q >> 3);  // 13-bit signed immediate offsets
+        asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
+                     : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+    }
+}
+// one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and bin L (the
+// same address on every lane) from rowL
+template <int E>
+__device__ __forceinline__ void gload_row(f2v (&v)[E + 1], const float2* rowlane, const float2* rowL) {
+    f2v (&head)[E] = *reinterpret_cast<f2v(*)[E]>(&v[0]);
+    gload_pairs<E>(head, reinterpret_cast<const float*>(rowlane));
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");
+}
+template <int K, int E>
+__device__ __forceinline__ void vm_wait(f2v (&xr)[E]) {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K) : "memory");
+#pragma unroll
+    for (int q = 0; q < E; ++q) asm volatile("" : "+v"(xr[q]));  // uses stay after the wait
+}
+
 __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
     float2 t;
     t.x = __builtin_fmaf(b.x, w.x, -(b.y * w.y));
@@ -146,14 +224,21 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
             for (int s = 0; s < R / 2; ++s) {
                 const int br = bitrevc(s & ((1 << st) - 1), st);
                 // pass 0: jm = 0, S = 1: compile-time index into the hoisted tw0 (SGPRs)
-                float2 w = (P == 0) ? tw0[(Ns - 1) + br] : tw[(Ns - 1) + jm + S * br];
-                if (INV) w.y = -w.y;
-                const float2 top = a[s];
-                const float2 t = cmul(a[s + R / 2], w);
-                b[2 * s].x = top.x + t.x;
-                b[2 * s].y = top.y + t.y;
-                b[2 * s + 1].x = top.x - t.x;
-                b[2 * s + 1].y = top.y - t.y;
+                // packed (v_pk_*) form of cmul + butterfly, same roundings as cmul();
+                // INV multiplies by conj(w)
+                const f2v top = f2v{a[s].x, a[s].y};
+                const f2v bot = f2v{a[s + R / 2].x, a[s + R / 2].y};
+                f2v t;
+                if constexpr (P == 0) {
+                    const float2 w = tw0[(Ns - 1) + br];
+                    t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
+                } else {
+                    const float2 w = lds_ld(&tw[(Ns - 1) + jm + S * br]);
+                    t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
+                }
+                const f2v u0 = top + t, u1 = top - t;
+                b[2 * s] = make_float2(u0.x, u0.y);
+                b[2 * s + 1] = make_float2(u1.x, u1.y);
             }
 #pragma unroll
             for (int q = 0; q < R; ++q) a[q] = b[q];
@@ -190,7 +275,7 @@ __device__ __forceinline__ void pass_load(float2 (&v)[Geo<L>::E], const float2* 
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
-        for (int q = 0; q < R; ++q) v[g * R + q] = base[G_::padc(64 * g + q * (L / R))];
+        for (int q = 0; q < R; ++q) v[g * R + q] = lds_ld(&base[G_::padc(64 * g + q * (L / R))]);
     }
 }
 

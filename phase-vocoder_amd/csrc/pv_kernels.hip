@@ -109,13 +109,13 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
     for (int c = 0; c < CH; ++c) {
         const int i = i0 + c;
         if (i < E) {
-            A[c] = baseA[G_::padc(64 * i)];
-            Bz[c] = (i == 0 && lane == 0) ? tile[0] : baseB[-G_::padc(64 * i)];
-            tw[c] = baseT[64 * i];
+            A[c] = lds_ld(&baseA[G_::padc(64 * i)]);
+            Bz[c] = lds_ld((i == 0 && lane == 0) ? tile : &baseB[-G_::padc(64 * i)]);
+            tw[c] = lds_ld(&baseT[64 * i]);
         } else {
-            A[c] = tile[0];
-            Bz[c] = tile[0];
-            tw[c] = twsl[L];
+            A[c] = lds_ld(tile);
+            Bz[c] = A[c];
+            tw[c] = lds_ld(&twsl[L]);
         }
     }
 #pragma unroll
@@ -146,7 +146,7 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
 // for its phase).  The unwrap decision m(t) = f(phi[t], phi[t-1]) is accumulated in
 // registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
 template <int L>
-__global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaParams p) {
+__global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -179,19 +179,24 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaPar
     PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; m0[i] = 0; })
 
     // One frame: window + FFT + split + atan2 (+ spectrum row, decisions) from raw samples.
-    auto frame = [&](int u, const float2 (&xr)[E]) {
-        const int t = t0 + u;
-        float2 z[E];
+    // One frame: window + FFT + split + atan2 (+ magnitude, unwrap decisions) into res.
+    // HALO (frame t0 - 1): phase only, it seeds phprev.
+    auto window = [&](const float2 (&xr)[E], float2 (&z)[E]) {
+        const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
 #pragma unroll
         for (int q = 0; q < E; ++q) {
-            const float2 wv = reinterpret_cast<const float2*>(winl)[lane + 64 * q];
+            const float2 wv = lds_ld(&wl[64 * q]);  // window samples 2 (lane + 64 q) + {0,1}
             z[q].x = xr[q].x * wv.x;
             z[q].y = xr[q].y * wv.y;
         }
+    };
+    auto frame = [&](int u, float2 (&z)[E], auto halo_tag) {
+        constexpr bool HALO = decltype(halo_tag)::value;
+        float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
+        (void)srow;
         fft_run<L, false>(z, tile, twl, tw0, lane);
         // bins in chunks of CH (bounded live registers), all reads of a chunk batched
         constexpr int CH = 3;
-        float2* srow = specc + (long long)t * p.spec_stride;
 #pragma unroll
         for (int i0 = 0; i0 <= E; i0 += CH) {
             float2 X[CH];
@@ -199,14 +204,15 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaPar
 #pragma unroll
             for (int c2 = 0; c2 < CH; ++c2) {
                 const int i = i0 + c2;
-                if (i > E || (i == E && lane != 0)) break;
+                if (i > E) break;
                 const int k = (i == E) ? L : lane + 64 * i;
                 const float ph = atan2_pv(X[c2].y, X[c2].x);
-                if (u >= 0) {
+                if constexpr (!HALO) {
                     const float mag = __builtin_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
-                    srow[k] = make_float2(mag, ph);
-                    const int m = unwrap_count(ph, phprev[i], ekl[k]);
-                    if (u == 0) m0[i] = m;
+                    // bin L (i = E) has the same value and address on every lane
+                    srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
+                    const int m = unwrap_count(ph, phprev[i], lds_ld(&ekl[k]));
+                    m0[i] = (u == 0) ? m : m0[i];
                     sacc[i] += (u == 0) ? 0 : m;
                 }
                 phprev[i] = ph;
@@ -214,36 +220,12 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaPar
         }
         wave_lds_sync();  // tile reads done before the next frame's pass_store
     };
-    const int u0 = (t0 > 0) ? -1 : 0;
-    // frames whose N samples are all inside [0, n) take the vector-load path with the raw
-    // samples fetched one frame ahead; the (at most N/hop) frames at the end of a channel
-    // take the bounds-checked path.
-    int ufast = u0;
-    if (p.aligned) {
-        const long long lastfull = (p.n - N) / p.hop;  // last frame index fully inside
-        ufast = (int)min((long long)nfr, max((long long)u0, lastfull - t0 + 1));
-    }
-    {
-        float2 xr[E];
-        if (u0 < ufast) {
-            const float* src = xc + (long long)(t0 + u0) * p.hop;
+    auto load_fast = [&](int u, float2 (&xr)[E]) {
+        const float* src = xc + (long long)(t0 + u) * p.hop;
 #pragma unroll
-            for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
-        }
-        for (int u = u0; u < ufast; ++u) {
-            float2 cur[E];
-#pragma unroll
-            for (int q = 0; q < E; ++q) cur[q] = xr[q];
-            if (u + 1 < ufast) {
-                const float* src = xc + (long long)(t0 + u + 1) * p.hop;
-#pragma unroll
-                for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
-            }
-            frame(u, cur);
-        }
-    }
-    for (int u = ufast; u < nfr; ++u) {
-        float2 xr[E];
+        for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
+    };
+    auto load_checked = [&](int u, float2 (&xr)[E]) {
         const long long base = (long long)(t0 + u) * p.hop;
 #pragma unroll
         for (int q = 0; q < E; ++q) {
@@ -251,7 +233,53 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : 2) void k_std_analysis(AnaPar
             xr[q].x = (s < p.n) ? xc[s] : 0.0f;
             xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
         }
-        frame(u, xr);
+    };
+    // frames whose N samples are all inside [0, n) take the vector-load path; the (at most
+    // N/hop) frames at the end of a channel take the bounds-checked path.
+    const long long lastfull = p.aligned ? (p.n - N) / p.hop : -1;  // last frame fully inside
+    if (t0 > 0) {
+        float2 xh[E], z[E];
+        if (t0 - 1 <= lastfull) load_fast(-1, xh); else load_checked(-1, xh);
+        window(xh, z);
+        frame(-1, z, std::true_type{});
+    }
+    const int ufast = (int)min((long long)nfr, max(0LL, lastfull - t0 + 1));
+    // steady state, trip u: [load x(u+1)] [compute frame u: E + 1 row stores]
+    // [vmcnt(E + 1): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
+    // The prefetch index is clamped (the last trip reloads its own frame), so the loads
+    // and stores are unconditional and the count is exact (gload_pairs / vm_wait).
+    if (L <= 1024 && ufast > 0) {
+        float2 z[E];
+        {
+            float2 xr[E];
+            load_fast(0, xr);
+            window(xr, z);
+        }
+        for (int u = 0; u < ufast; ++u) {
+            f2v xv[E];
+            gload_pairs<E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
+            frame(u, z, std::false_type{});  // exactly E + 1 row stores
+            vm_wait<E + 1>(xv);
+            float2 xr[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) xr[q] = make_float2(xv[q].x, xv[q].y);
+            window(xr, z);
+        }
+    } else if (ufast > 0) {  // L = 2048: compiler-tracked prefetch (the kernel uses AGPRs)
+        float2 xr[E];
+        load_fast(0, xr);
+        for (int u = 0; u < ufast; ++u) {
+            float2 z[E];
+            window(xr, z);
+            load_fast(min(u + 1, ufast - 1), xr);
+            frame(u, z, std::false_type{});
+        }
+    }
+    for (int u = ufast; u < nfr; ++u) {
+        float2 xr[E], z[E];
+        load_checked(u, xr);
+        window(xr, z);
+        frame(u, z, std::false_type{});
     }
     if (p.runsum != nullptr) {
         int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * BP;
@@ -379,34 +407,39 @@ __global__ __launch_bounds__(256) void k_carry(ScanParams p) {
 
 // ------------------------------------------------------------------ K3 synthesis
 // One wave = one run of F frames (virtually padded to F: frames >= `frames` are zero).
-// MODE 0/2: STANDARD time stretch / pitch shift — output phase rho*(phi + 2 pi (M_dec + (t+1) j_k)),
-//         Hann synthesis window with overlap normalisation folded into gain[].
+// MODE 0/2: STANDARD time stretch / pitch shift — output phase
+//         rho*(phi + 2 pi (M_dec + (t+1) j_k)), Hann synthesis window with
+//         the overlap normalisation folded into gain[].
 // MODE 1: REF_COMPAT — kernel.cu:352-432: x' = m cos(phi), y' = x' sin(phi), C2R N, /N,
 //         swap halves (rot = N/2), Hamming window (gain = w/N).
 // Overlap-add: a position is final once the frame that starts after it has been added;
 // final samples are stored straight to `out`.
-//   ROLA (out hop a multiple of 128, L <= 1024): in registers.  After the inverse FFT's last
-//     pass lane holds points lane + 64 c, i.e. samples 2 lane + {0,1} + 128 c, so every
-//     position a lane ever touches is congruent to 2 lane (+1) mod 128: the accumulator
-//     acc[c] covers run positions u*hs + 128 c + 2 lane + {0,1}; per frame the oldest
-//     hs/128 slots are stored and the rest shift down.  No LDS ring, no final FFT store.
-//   otherwise: per-wave LDS ring of N samples.
+//   DT > 0 (out hop = 128 DT, L <= 1024): in registers.  After the inverse FFT's last pass
+//     lane holds points lane + 64 c, i.e. samples 2 lane + {0,1} + 128 c, so every
+//     position a lane ever touches is congruent to 2 lane (+1) mod 128: acc[c] covers run
+//     positions u*hs + 128 c + 2 lane + {0,1}; per frame the oldest DT slots are stored
+//     and the rest shift down.  No LDS ring, no final FFT store.  Runs away from the ends
+//     of the output take a loop with unconditional stores and a self-tracked prefetch
+//     of the next spectrum row (gload_pairs / vm_wait, pv_device.hpp).
+//   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
-template <int L, int MODE, bool ROLA>
+template <int L, int MODE, int DT>
 __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
+    constexpr bool ROLA = DT > 0;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int SPW = N / 64;  // samples per lane per frame
     constexpr int B = L + 1;
+    constexpr bool GREG = ROLA && L <= 512;  // ROLA gains in registers (else LDS float2 reads)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* twl = reinterpret_cast<float2*>(smem);                     // L
     float2* twsl = twl + L;                                            // L (+2 pad)
     float2* tiles = twsl + (L + 2);                                    // 4 x TILE
     float* rings = reinterpret_cast<float*>(tiles + 4 * G_::TILE);    // 4 x N
-    float* gainl = rings + 4 * N;                                      // N (ring path)
-    float* ekl = gainl + ((ROLA && L <= 512) ? 0 : N);                 // B (+pad)
+    float* gainl = rings + 4 * N;                                      // N (unless GREG)
+    float* ekl = gainl + (GREG ? 0 : N);                               // B (+pad)
     unsigned* jkl = reinterpret_cast<unsigned*>(ekl + (B + 3));        // B (+pad)
     int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
     const int hs = p.hs;
@@ -416,7 +449,6 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) { twl[i] = p.tw[i]; twsl[i] = p.tws[i]; }
-    constexpr bool GREG = ROLA && L <= 512;  // ROLA gains in registers (else LDS float2 reads)
     if (!GREG)
         for (int i = tid; i < N; i += 256) gainl[i] = p.gain[i];
     if (MODE != 1) {
@@ -451,8 +483,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
 
     // ROLA state: acc[c] = run positions u*hs + 128 c + 2 lane + {0,1}; gains likewise
     constexpr int NS = ROLA ? E : 1;
+    constexpr int D = ROLA ? DT : 1;  // slots completed per frame (ROLA)
     float2 acc[NS], gn[GREG ? NS : 1];
-    const int D = hs >> 7;  // slots completed per frame (ROLA)
     if (ROLA) {
         const float2* g2 = reinterpret_cast<const float2*>(p.gain);
 #pragma unroll
@@ -462,175 +494,218 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
         }
     }
 
-    float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
-    if (nfr > 0) {
-        const float2* srow = specc + (long long)t0 * p.spec_stride;
-        PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-    }
-    for (int u = 0; u < p.F; ++u) {
-        const int t = t0 + u;
-        if (u < nfr) {
-            float mag[E + 1], ph[E + 1];
-            PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
-            if (u + 1 < nfr) {
-                const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
-                PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-            }
-            if (MODE != 1) {
-                const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
-                float phc[E + 1];
-                float ekv[E + 1];
-                unsigned jkv[E + 1];
-                PV_FOR_BINS(E, lane, { ekv[i] = ekl[k]; jkv[i] = jkl[k]; })
+    // One frame t = t0 + u from its spectrum row sv (mag, phase of this lane's bins):
+    // phase processing, C2R pre-split, inverse FFT.  ROLA: result left in z (last-pass
+    // register layout); ring path: result in tile.
+    auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
+        float mag[E + 1], ph[E + 1];
+        PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
+        if constexpr (MODE != 1) {
+            const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
+            float phc[E + 1];
+            float ekv[E + 1];
+            unsigned jkv[E + 1];
+            PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
+            PV_FOR_BINS(E, lane, {
+                const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
+                M[i] += (u > 0) ? mm : 0;
+                phprev[i] = ph[i];
+            })
+            // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
+            // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
+            const unsigned qq = (unsigned)p.q, pm = (unsigned)p.p_mod;
+            if (p.q_pow2) {
                 PV_FOR_BINS(E, lane, {
-                    const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
-                    M[i] += (u > 0) ? mm : 0;
-                    phprev[i] = ph[i];
+                    const unsigned x = pm * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
+                    phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * p.inv_q));
                 })
-                // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
-                // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
-                const unsigned qq = (unsigned)p.q, pm = (unsigned)p.p_mod;
-                if (p.q_pow2) {
-                    PV_FOR_BINS(E, lane, {
-                        const unsigned x = pm * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
-                        phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * p.inv_q));
-                    })
-                } else {
-                    PV_FOR_BINS(E, lane, {
-                        int mdq = M[i] % (int)qq;
-                        mdq += (mdq < 0) ? (int)qq : 0;
-                        const unsigned x = pm * (unsigned)mdq + tq * jkv[i];
-                        phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x % qq) * p.inv_q));
-                    })
-                }
-                if constexpr (MODE == 2) {
-                    float2 Y[E + 1];
-                    PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
-                    wave_lds_sync();
-                    PV_FOR_BINS(E, lane, {
-                        const int s = srcl[k];
-                        float ms = 0.0f, pc = 0.0f;
-                        if (s >= 0) {
-                            const int cnt = srcl[B + k];
-                            pc = tile[G_::pad(s)].y;
-                            for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
-                        }
-                        float sn, cs;
-                        sincos_pv(pc, &sn, &cs);
-                        Y[i] = make_float2(ms * cs, ms * sn);
-                    })
-                    wave_lds_sync();
-                    PV_FOR_BINS(E, lane, {
-                        float2 y = Y[i];
-                        if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
-                        tile[G_::pad(k)] = y;
-                    })
-                } else {
-                    PV_FOR_BINS(E, lane, {
-                        float sn, cs;
-                        sincos_pv(phc[i], &sn, &cs);
-                        float2 y = make_float2(mag[i] * cs, mag[i] * sn);
-                        if (k == 0 || k == L) y.y = 0.0f;
-                        tile[G_::pad(k)] = y;
-                    })
-                }
+            } else {
+                PV_FOR_BINS(E, lane, {
+                    int mdq = M[i] % (int)qq;
+                    mdq += (mdq < 0) ? (int)qq : 0;
+                    const unsigned x = pm * (unsigned)mdq + tq * jkv[i];
+                    phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x % qq) * p.inv_q));
+                })
+            }
+            if constexpr (MODE == 2) {
+                float2 Y[E + 1];
+                PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
+                wave_lds_sync();
+                PV_FOR_BINS(E, lane, {
+                    const int s = srcl[k];
+                    float ms = 0.0f, pc = 0.0f;
+                    if (s >= 0) {
+                        const int cnt = srcl[B + k];
+                        pc = tile[G_::pad(s)].y;
+                        for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
+                    }
+                    float sn, cs;
+                    sincos_pv(pc, &sn, &cs);
+                    Y[i] = make_float2(ms * cs, ms * sn);
+                })
+                wave_lds_sync();
+                PV_FOR_BINS(E, lane, {
+                    float2 y = Y[i];
+                    if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
+                    tile[G_::pad(k)] = y;
+                })
             } else {
                 PV_FOR_BINS(E, lane, {
                     float sn, cs;
-                    sincos_pv(ph[i], &sn, &cs);
-                    const float xr = mag[i] * cs;                 // kernel.cu:127
-                    float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
+                    sincos_pv(phc[i], &sn, &cs);
+                    float2 y = make_float2(mag[i] * cs, mag[i] * sn);
                     if (k == 0 || k == L) y.y = 0.0f;
                     tile[G_::pad(k)] = y;
                 })
             }
-            wave_lds_sync();
-            // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
-            float2 z[E];
-            const float2* baseA = tile + G_::pad(lane);
-            const float2* baseB = tile + G_::pad(L - lane);
+        } else {
+            PV_FOR_BINS(E, lane, {
+                float sn, cs;
+                sincos_pv(ph[i], &sn, &cs);
+                const float xr = mag[i] * cs;                 // kernel.cu:127
+                float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
+                if (k == 0 || k == L) y.y = 0.0f;
+                tile[G_::pad(k)] = y;
+            })
+        }
+        wave_lds_sync();
+        // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
+        const float2* baseA = tile + G_::pad(lane);
+        const float2* baseB = tile + G_::pad(L - lane);
 #pragma unroll
-            for (int q = 0; q < E; ++q) {
-                const int i = lane + 64 * q;
-                const float2 A = baseA[G_::padc(64 * q)];
-                const float2 Bc = baseB[-G_::padc(64 * q)];
-                const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
-                const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
-                const float2 tw = twsl[i];                       // e^{-2 pi i k/N}
-                const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
-                const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
-                z[q] = make_float2(fer - Foi, fei + For);
-            }
-            wave_lds_sync();
-            if constexpr (ROLA) {
-                fft_run<L, true, false>(z, tile, twl, tw0, lane);
-                // register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
-                // moves raw slot cr to OLA slot cr + E/2 (mod E)
+        for (int q = 0; q < E; ++q) {
+            const int i = lane + 64 * q;
+            const float2 A = lds_ld(&baseA[G_::padc(64 * q)]);
+            const float2 Bc = lds_ld(&baseB[-G_::padc(64 * q)]);
+            const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
+            const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
+            const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
+            const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
+            const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
+            z[q] = make_float2(fer - Foi, fei + For);
+        }
+        wave_lds_sync();
+        if constexpr (ROLA) fft_run<L, true, false>(z, tile, twl, tw0, lane);
+        else fft_run<L, true>(z, tile, twl, tw0, lane);
+    };
+    // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
+    // moves raw slot cr to OLA slot cr + E/2 (mod E)
+    auto ola_regs = [&](const float2 (&z)[E]) {
 #pragma unroll
-                for (int idx = 0; idx < E; ++idx) {
-                    const int cr = last_slot<L>(idx);
-                    const int cs = (MODE == 1) ? ((cr + E / 2) & (E - 1)) : cr;
-                    const float2 g = GREG ? gn[GREG ? cs : 0]
-                                          : reinterpret_cast<const float2*>(gainl)[64 * cs + lane];
-                    acc[cs].x = __builtin_fmaf(z[idx].x, g.x, acc[cs].x);
-                    acc[cs].y = __builtin_fmaf(z[idx].y, g.y, acc[cs].y);
-                }
+        for (int idx = 0; idx < E; ++idx) {
+            const int cr = last_slot<L>(idx);
+            const int cs = (MODE == 1) ? ((cr + E / 2) & (E - 1)) : cr;
+            const float2 g = GREG ? gn[GREG ? cs : 0]
+                                  : lds_ld(reinterpret_cast<const float2*>(gainl) + 64 * cs + lane);
+            acc[cs].x = __builtin_fmaf(z[idx].x, g.x, acc[cs].x);
+            acc[cs].y = __builtin_fmaf(z[idx].y, g.y, acc[cs].y);
+        }
+    };
+    // ROLA flush of frame u: positions [u*hs, (u+1)*hs) = slots 0..D-1 are final
+    auto flush_regs = [&](int u, auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        const long long pb = obase + (long long)u * hs + 2 * lane;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const long long gp = pb + 128 * d;
+            if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
+                *reinterpret_cast<float2*>(outc + gp) = acc[d];
             } else {
-                fft_run<L, true>(z, tile, twl, tw0, lane);
-                // overlap-add the frame into the ring (lane-distinct positions)
-                // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
-                // 2 pad(nn >> 1) + (nn & 1) = per-lane base + compile-time offset
-                constexpr int ROT = (MODE == 1) ? N / 2 : 0;
-                const float* ty = reinterpret_cast<const float*>(tile) + 2 * G_::pad(lane >> 1) + (lane & 1);
-                const int rbase = u * hs + lane;
+                if (gp < p.out_len) outc[gp] = acc[d].x;
+                if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
+            }
+        }
 #pragma unroll
-                for (int i = 0; i < SPW; ++i) {
-                    const int n = lane + 64 * i;
-                    const int c = ((64 * i + ROT) & (N - 1)) >> 1;
-                    const float yv = ty[2 * G_::padc(c)];
-                    const int pos = (rbase + 64 * i) & (N - 1);
-                    ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
+        for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
+    };
+
+    // the self-tracked prefetch needs registers that are never spilled or copied while the
+    // loads are in flight: only at L <= 512, where the kernels fit without spills
+    constexpr bool FASTOK = ROLA && L <= 512;
+    const bool fast = FASTOK && nfr == p.F && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
+    if (FASTOK && fast) {
+        // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
+        // [vmcnt(D): row u+1 landed, the stores may still be in flight]
+        float2 sv[E + 1];
+        {
+            const float2* srow = specc + (long long)t0 * p.spec_stride;
+#pragma unroll
+            for (int i = 0; i < E; ++i) sv[i] = srow[lane + 64 * i];
+            sv[E] = srow[L];
+        }
+        for (int u = 0; u < p.F; ++u) {
+            f2v nx[E + 1];
+            const float2* nrow = specc + (long long)(t0 + min(u + 1, p.F - 1)) * p.spec_stride;
+            gload_row<E>(nx, nrow + lane, nrow + L);
+            float2 z[E];
+            synth(u, t0 + u, sv, z);
+            ola_regs(z);
+            flush_regs(u, std::true_type{});  // exactly D stores
+            vm_wait<D>(nx);
+#pragma unroll
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(nx[i].x, nx[i].y);
+        }
+    } else {
+        float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
+        if (nfr > 0) {
+            const float2* srow = specc + (long long)t0 * p.spec_stride;
+            PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
+        }
+        for (int u = 0; u < p.F; ++u) {
+            const int t = t0 + u;
+            if (u < nfr) {
+                float2 cur[E + 1];
+#pragma unroll
+                for (int i = 0; i <= E; ++i) cur[i] = sv[i];
+                if (u + 1 < nfr) {
+                    const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
+                    PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
+                }
+                float2 z[E];
+                synth(u, t, cur, z);
+                if constexpr (ROLA) {
+                    ola_regs(z);
+                } else {
+                    // overlap-add the frame into the ring (lane-distinct positions)
+                    // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
+                    // 2 pad(nn >> 1) + (nn & 1) = per-lane base + compile-time offset
+                    constexpr int ROT = (MODE == 1) ? N / 2 : 0;
+                    const float* ty = reinterpret_cast<const float*>(tile) + 2 * G_::pad(lane >> 1) + (lane & 1);
+                    const int rbase = u * hs + lane;
+#pragma unroll
+                    for (int i = 0; i < SPW; ++i) {
+                        const int n = lane + 64 * i;
+                        const int cc = ((64 * i + ROT) & (N - 1)) >> 1;
+                        const float yv = ty[2 * G_::padc(cc)];
+                        const int pos = (rbase + 64 * i) & (N - 1);
+                        ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
+                    }
+                    wave_lds_sync();
+                }
+            }
+            if constexpr (ROLA) {
+                flush_regs(u, std::false_type{});
+            } else {
+                // positions [u*hs, (u+1)*hs) are final for this run
+                for (int j = lane; j < hs; j += 64) {
+                    const int pl = u * hs + j;
+                    const int slot = pl & (N - 1);
+                    const float v = ring[slot];
+                    ring[slot] = 0.0f;
+                    if (obase + pl < p.out_len) outc[obase + pl] = v;
                 }
                 wave_lds_sync();
             }
         }
-        if constexpr (ROLA) {
-            // positions [u*hs, (u+1)*hs) = slots 0..D-1 are final: store, shift down
-            const long long pb = obase + (long long)u * hs + 2 * lane;
-            for (int d = 0; d < D; ++d) {
-                const long long gp = pb + 128 * d;
-                if (p.out_aligned && gp + 1 < p.out_len) {
-                    *reinterpret_cast<float2*>(outc + gp) = acc[0];
-                } else {
-                    if (gp < p.out_len) outc[gp] = acc[0].x;
-                    if (gp + 1 < p.out_len) outc[gp + 1] = acc[0].y;
-                }
-#pragma unroll
-                for (int s = 0; s + 1 < NS; ++s) acc[s] = acc[s + 1];
-                acc[NS - 1] = make_float2(0.0f, 0.0f);
-            }
-        } else {
-            // positions [u*hs, (u+1)*hs) are final for this run
-            for (int j = lane; j < hs; j += 64) {
-                const int pl = u * hs + j;
-                const int slot = pl & (N - 1);
-                const float v = ring[slot];
-                ring[slot] = 0.0f;
-                if (obase + pl < p.out_len) outc[obase + pl] = v;
-            }
-            wave_lds_sync();
-        }
     }
     if constexpr (ROLA) {
-        // the run's tail (positions F*hs + j, j < N - hs) -> ring[j]; ring index of tail
-        // position j below is then (F*hs + j) & (N-1) rewritten as j via tail_at()
+        // the run's tail (positions F*hs + j, j < N - hs) -> ring[j]
         float2* r2 = reinterpret_cast<float2*>(ring);
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
-            if (s < NS - D) r2[64 * s + lane] = acc[s];
+        for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
     }
     __syncthreads();
-    // seams: run w's tail (ring positions [F*hs, F*hs + TL)) overlaps run w+1's head
+    // seams: run w's tail (positions F*hs + j) overlaps run w+1's head
     if (w > 0) {
         const float* prev = rings + (w - 1) * N;
         for (int j = lane; j < TL; j += 64) {
@@ -700,25 +775,29 @@ template <int L>
 static size_t ana_lds_compat() {
     return sizeof(float2) * (L + 4 * Geo<L>::TILE);
 }
-// twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with ROLA at L <= 512
-// the gains live in registers and gainl is not allocated (it is the last float array before ekl,
-// so ekl/jkl/srcl simply start N floats earlier: see the kernel's carve-up)
+// twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with register
+// overlap-add at L <= 512 the gains live in registers and gainl is not allocated
 template <int L>
-static size_t syn_lds(bool rola) {
+static size_t syn_lds(int dt) {
     return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) +
-           sizeof(float) * ((rola && L <= 512) ? 4 : 5) * (2 * L) + sizeof(float) * 4 * (L + 1 + 3);
+           sizeof(float) * ((dt > 0 && L <= 512) ? 4 : 5) * (2 * L) + sizeof(float) * 4 * (L + 1 + 3);
 }
 
-static bool syn_rola(int L, int hs) { return (hs % 128 == 0) && L <= 1024; }
+// register overlap-add slots per frame (out hop = 128 DT), 0 = LDS ring
+static int syn_dt(int L, int hs) {
+    if (L > 1024 || hs % 128 != 0) return 0;
+    const int d = hs / 128;
+    return (d == 1 || d == 2 || d == 4) ? d : 0;
+}
 
 size_t synthesis_lds_bytes(int L, int hs) {
-    const bool r = syn_rola(L, hs);
+    const int dt = syn_dt(L, hs);
     switch (L) {
-        case 128: return syn_lds<128>(r);
-        case 256: return syn_lds<256>(r);
-        case 512: return syn_lds<512>(r);
-        case 1024: return syn_lds<1024>(r);
-        case 2048: return syn_lds<2048>(r);
+        case 128: return syn_lds<128>(dt);
+        case 256: return syn_lds<256>(dt);
+        case 512: return syn_lds<512>(dt);
+        case 1024: return syn_lds<1024>(dt);
+        case 2048: return syn_lds<2048>(dt);
     }
     return 0;
 }
@@ -761,24 +840,34 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int MODE>
+static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParams& p, hipStream_t s) {
+#define PV_SYN_DT(LL_)                                                                         \
+    switch (dt) {                                                                              \
+        case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
+        case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
+        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
+        default: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0>), grid, dim3(256), syn_lds<LL_>(0), s, p); break; \
+    }
+    switch (L) {
+        case 128: PV_SYN_DT(128); break;
+        case 256: PV_SYN_DT(256); break;
+        case 512: PV_SYN_DT(512); break;
+        case 1024: PV_SYN_DT(1024); break;
+        case 2048: hipLaunchKernelGGL((k_synthesis<2048, MODE, 0>), grid, dim3(256), syn_lds<2048>(0), s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef PV_SYN_DT
+    return hipGetLastError();
+}
+
+// mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
-    const bool rola = syn_rola(L, p.hs);
-#define PV_SYN(M_, R_)                                                                   \
-    PV_DISPATCH_L(L, {                                                                   \
-        hipLaunchKernelGGL((k_synthesis<LL, M_, R_ && (LL <= 1024)>), grid, dim3(256),   \
-                           syn_lds<LL>(R_ && (LL <= 1024)), s, p);                      \
-    })
-    // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
-    if (mode == 0) {
-        if (rola) { PV_SYN(0, true); } else { PV_SYN(0, false); }
-    } else if (mode == 2) {
-        if (rola) { PV_SYN(2, true); } else { PV_SYN(2, false); }
-    } else {
-        if (rola) { PV_SYN(1, true); } else { PV_SYN(1, false); }
-    }
-#undef PV_SYN
-    return hipGetLastError();
+    const int dt = syn_dt(L, p.hs);
+    if (mode == 0) return launch_synthesis_mode<0>(L, dt, grid, p, s);
+    if (mode == 2) return launch_synthesis_mode<2>(L, dt, grid, p, s);
+    return launch_synthesis_mode<1>(L, dt, grid, p, s);
 }
 
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s) {

@@ -71,3 +71,37 @@ def test_product_does_not_reference_oracle():
                 txt = "\n".join(code)
                 for bad in ("import pvref", "from pvref", "libpvref", "oracle/", "pvr_"):
                     assert bad not in txt, (f, bad)
+
+
+@pytest.mark.slow
+def test_prefetch_kernels_have_no_spills():
+    """The self-tracked prefetch (gload_pairs / vm_wait, pv_device.hpp) is only sound when
+    the registers it loads are never spilled or moved to AGPRs while in flight: the
+    kernels that use it (analysis L <= 1024, register-OLA synthesis L <= 512) must compile
+    without spills or AGPR use."""
+    import re
+    import subprocess
+    csrc = os.path.join(_lib.ROOT, "phase-vocoder_amd", "csrc")
+    r = subprocess.run(["make", "-s", "-C", csrc, "resource-usage"], capture_output=True, text=True,
+                       timeout=900)
+    rows, cur = {}, None
+    for line in (r.stdout + r.stderr).splitlines():
+        m = re.search(r"remark:\s+(.*?)\s*\[-Rpass", line)
+        if not m:
+            continue
+        body = m.group(1)
+        if body.startswith("Function Name:"):
+            cur = body.split(":", 1)[1].strip()
+            rows[cur] = {}
+        elif cur and ":" in body:
+            k, v = body.split(":", 1)
+            rows[cur][k.strip()] = v.strip()
+    assert rows, r.stderr[-2000:]
+    checked = 0
+    for name, info in rows.items():
+        m = re.match(r"_ZN2pv14k_std_analysisILi(\d+)E", name)
+        n = re.match(r"_ZN2pv11k_synthesisILi(\d+)ELi\dELi([124])E", name)
+        if (m and int(m.group(1)) <= 1024) or (n and int(n.group(1)) <= 512):
+            checked += 1
+            assert info.get("VGPRs Spill") == "0" and info.get("AGPRs") == "0", (name, info)
+    assert checked >= 4 + 3 * 3 * 3
