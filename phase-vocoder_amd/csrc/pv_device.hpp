@@ -116,9 +116,8 @@ __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
 // atan2 of the contract (oracle pvr_atan2f); atan(a) = a*P(a^2), |err| <= 2.7e-7 rad.
 __device__ __forceinline__ float atan2_pv(float y, float x) {
     float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
-    bool xg = ax > ay;
-    float mx = xg ? ax : ay;
-    float mn = xg ? ay : ax;
+    float mx = __builtin_fmaxf(ax, ay);  // = (ax > ay ? ax : ay) for non-NaN |x|, |y|
+    float mn = __builtin_fminf(ax, ay);
     float a = mn / mx;  // IEEE division (-fhip-fp32-correctly-rounded-divide-sqrt)
     float s = a * a;
     float p = -0x1.8ba68ap-10f;

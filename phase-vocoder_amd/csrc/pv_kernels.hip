@@ -208,7 +208,9 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
                 const int k = (i == E) ? L : lane + 64 * i;
                 const float ph = atan2_pv(X[c2].y, X[c2].x);
                 if constexpr (!HALO) {
-                    const float mag = __builtin_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
+                    // the phase, which drives the unwrap decisions, stays bit-exact
+                    const float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                     // bin L (i = E) has the same value and address on every lane
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
                     const int m = unwrap_count(ph, phprev[i], lds_ld(&ekl[k]));
