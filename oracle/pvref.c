@@ -103,7 +103,8 @@ void pvr_fft_c32(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* tw, int inve
      * v1 = in[j+L/2]*W(j%Ns), out[expand(j,Ns,2)+{0,Ns}] = v0 +- v1), with the twiddle
      * W(idx,Ns) = e^{-i pi idx/Ns} taken from the table tw[idx*L/(2Ns)] instead of being
      * recomputed with cos/sin per butterfly.  The top element is never multiplied; the
-     * bottom one always is (also by W = 1). */
+     * bottom one is, except in the first two stages where W is exactly 1 (Ns = 1, and
+     * Ns = 2, idx = 0: t = b) or -i (Ns = 2, idx = 1: t = (b.y, -b.x); +i when inverse). */
     pvr_c32* in = data;
     pvr_c32* out = tmp;
     const int half = L / 2;
@@ -114,7 +115,15 @@ void pvr_fft_c32(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* tw, int inve
             int idx = j & (Ns - 1);
             pvr_c32 w = tw[idx * tstride];
             if (inverse) w.y = -w.y;
-            pvr_c32 t = cmul_c(b, w);
+            pvr_c32 t;
+            if (Ns == 1 || (Ns == 2 && idx == 0)) {
+                t = b;
+            } else if (Ns == 2) {
+                t.x = inverse ? -b.y : b.y;
+                t.y = inverse ? b.x : -b.x;
+            } else {
+                t = cmul_c(b, w);
+            }
             int pos = (j / Ns) * 2 * Ns + idx;
             out[pos].x = a.x + t.x;
             out[pos].y = a.y + t.y;

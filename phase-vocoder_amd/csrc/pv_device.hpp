@@ -228,7 +228,14 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                 const f2v top = f2v{a[s].x, a[s].y};
                 const f2v bot = f2v{a[s + R / 2].x, a[s + R / 2].y};
                 f2v t;
-                if constexpr (P == 0) {
+                if (Ns == 1) {
+                    t = bot;  // W = 1 exactly (fp32 contract)
+                } else if (Ns == 2) {
+                    // W = 1 (idx 0) or exactly -i (idx 1; +i when INV): a swap and a sign
+                    const f2v r = INV ? f2v{-bot.y, bot.x} : f2v{bot.y, -bot.x};
+                    const int idx = (P == 0) ? br : jm;
+                    t = (idx != 0) ? r : bot;
+                } else if constexpr (P == 0) {
                     const float2 w = tw0[(Ns - 1) + br];
                     t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
                 } else {
