@@ -389,8 +389,11 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         return fail(PV_ERR_UNSUPPORTED, "FFT length outside [128, 2048]");
     }
     h->tail_len = N - h->hs;
-    // frames per wave-run; a run's output span must cover the overlap tail
-    int F = 16;
+    // frames per wave-run: longer runs amortise the halo frame each run transforms (1/F of
+    // the analysis work) as long as the batch still yields >= 2048 workgroups of 4 runs;
+    // a run's output span must cover the overlap tail
+    const long long work = (long long)std::max(cfg->max_channels, 1) * std::max(cfg->max_frames, 1);
+    int F = (work >= 2048LL * 4 * 32) ? 32 : (work >= 1024LL * 4 * 16) ? 16 : 8;
     while ((long long)F * h->hs < h->tail_len) F += 4;
     h->F = F;
     h->max_runs = (cfg->max_frames + F - 1) / F;
