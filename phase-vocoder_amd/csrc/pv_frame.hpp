@@ -1,0 +1,204 @@
+// pv_frame.hpp — per-frame building blocks shared by the batched kernels (pv_kernels.hip)
+// and the real-time kernel (pv_rt.hip): the real-FFT split of the analysis transform and
+// the whole synthesis of one frame (phase propagation -> polar->rect -> C2R pre-split ->
+// inverse FFT).
+#pragma once
+#include "pv_device.hpp"
+
+namespace pv {
+
+// Real-FFT split of bin k (0 <= k <= L) from the natural-order L-point transform in tile.
+template <int L>
+__device__ __forceinline__ float2 real_split(const float2* tile, const float2* __restrict__ tws, int k) {
+    using G_ = Geo<L>;
+    const float2 A = tile[G_::pad(k & (L - 1))];
+    const float2 Bz = tile[G_::pad((L - k) & (L - 1))];
+    const float er = 0.5f * (A.x + Bz.x);
+    const float ei = 0.5f * (A.y - Bz.y);
+    const float orr = 0.5f * (A.y + Bz.y);
+    const float oi = 0.5f * (Bz.x - A.x);
+    const float2 tw = tws[k];
+    float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
+    float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
+    if (k == 0 || k == L) Xi = 0.0f;
+    return make_float2(Xr, Xi);
+}
+
+// Bins i0 .. i0+CH-1 of a lane (reads batched; entries past E are dummies).
+template <int L, int CH>
+__device__ __forceinline__ void split_chunk(const float2* tile, const float2* twsl, int lane, int i0,
+                                            float2 (&X)[CH]) {
+    using G_ = Geo<L>;
+    constexpr int E = G_::E;
+    // A = Z[k], B = Z[(L-k) mod L], k = lane + 64 i: affine in i from two per-lane bases;
+    // only (lane 0, i = 0) wraps (B = Z[0]) and bin L (i = E, lane 0) uses Z[0] twice.
+    const float2* baseA = tile + G_::pad(lane);
+    const float2* baseB = tile + G_::pad(L - lane);
+    const float2* baseT = twsl + lane;
+    float2 A[CH], Bz[CH], tw[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        if (i < E) {
+            A[c] = lds_ld(&baseA[G_::padc(64 * i)]);
+            Bz[c] = lds_ld((i == 0 && lane == 0) ? tile : &baseB[-G_::padc(64 * i)]);
+            tw[c] = lds_ld(&baseT[64 * i]);
+        } else {
+            A[c] = lds_ld(tile);
+            Bz[c] = A[c];
+            tw[c] = lds_ld(&twsl[L]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        const float er = 0.5f * (A[c].x + Bz[c].x);
+        const float ei = 0.5f * (A[c].y - Bz[c].y);
+        const float orr = 0.5f * (A[c].y + Bz[c].y);
+        const float oi = 0.5f * (Bz[c].x - A[c].x);
+        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
+        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
+        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
+        X[c] = make_float2(Xr, Xi);
+    }
+}
+
+// bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
+#define PV_FOR_BINS(E_, lane_, ...)                              \
+    _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \
+        if (i == (E_) && (lane_) != 0) break;                    \
+        const int k = (i == (E_)) ? 64 * (E_) : (lane_) + 64 * i; \
+        (void)k;                                                 \
+        __VA_ARGS__                                              \
+    }
+
+
+// STANDARD phase propagation constants: phi_s = rho phi + 2 pi ((p M_tot) mod q) / q,
+// M_tot = M_dec + (t+1) j_k
+struct PhaseMap {
+    float rho;
+    unsigned q, p_mod;
+    int q_pow2;
+    float inv_q;
+};
+
+// LDS tables of the synthesis side (see the kernels' carve-up)
+struct SynLds {
+    const float2* twl;    // stage-major twiddles, L-point
+    const float2* twsl;   // e^{-2 pi i k/N}, k <= L
+    const float* ekl;     // expected advance e_k (STANDARD)
+    const unsigned* jkl;  // (p j_k) mod q (STANDARD)
+    const int* srcl;      // pitch map: first source bin [B], source count [B] (MODE 2)
+};
+
+// One synthesis frame from the spectrum row sv (mag, phase of the lane's bins k = lane +
+// 64 i, i < E, and k = L on lane 0).  MODE 0/2 STANDARD stretch/pitch (unwrap state M,
+// phprev updated; add_decision = false for a run's first frame, whose decision the carry
+// already holds), MODE 1 REF_COMPAT (kernel.cu:121-129 y-bug).  tq = (t + 1) mod q.
+// Result: STORE_LAST: time samples in tile (natural order, padded); else the inverse
+// FFT's last-pass registers z (point lane + 64 last_slot(idx)).
+template <int L, int MODE, bool STORE_LAST>
+__device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
+                                            unsigned tq, int (&M)[Geo<L>::E + 1],
+                                            float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
+                                            const SynLds& tb, const float2 (&tw0)[Geo<L>::E],
+                                            float2* tile, int lane, float2 (&z)[Geo<L>::E]) {
+    using G_ = Geo<L>;
+    constexpr int E = G_::E;
+    constexpr int B = L + 1;
+    const float2* twl = tb.twl;
+    const float2* twsl = tb.twsl;
+    const float* ekl = tb.ekl;
+    const unsigned* jkl = tb.jkl;
+    const int* srcl = tb.srcl;
+    (void)ekl; (void)jkl; (void)srcl; (void)B;
+    float mag[E + 1], ph[E + 1];
+    PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
+    if constexpr (MODE != 1) {
+        float phc[E + 1];
+        float ekv[E + 1];
+        unsigned jkv[E + 1];
+        PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
+        PV_FOR_BINS(E, lane, {
+            const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
+            M[i] += add_decision ? mm : 0;
+            phprev[i] = ph[i];
+        })
+        // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
+        // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
+        const unsigned qq = pm.q, pmod = pm.p_mod;
+        if (pm.q_pow2) {
+            PV_FOR_BINS(E, lane, {
+                const unsigned x = pmod * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
+                phc[i] = __builtin_fmaf(pm.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * pm.inv_q));
+            })
+        } else {
+            PV_FOR_BINS(E, lane, {
+                int mdq = M[i] % (int)qq;
+                mdq += (mdq < 0) ? (int)qq : 0;
+                const unsigned x = pmod * (unsigned)mdq + tq * jkv[i];
+                phc[i] = __builtin_fmaf(pm.rho, ph[i], kTwoPi * ((float)(x % qq) * pm.inv_q));
+            })
+        }
+        if constexpr (MODE == 2) {
+            float2 Y[E + 1];
+            PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
+            wave_lds_sync();
+            PV_FOR_BINS(E, lane, {
+                const int s = srcl[k];
+                float ms = 0.0f, pc = 0.0f;
+                if (s >= 0) {
+                    const int cnt = srcl[B + k];
+                    pc = tile[G_::pad(s)].y;
+                    for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
+                }
+                float sn, cs;
+                sincos_pv(pc, &sn, &cs);
+                Y[i] = make_float2(ms * cs, ms * sn);
+            })
+            wave_lds_sync();
+            PV_FOR_BINS(E, lane, {
+                float2 y = Y[i];
+                if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
+                tile[G_::pad(k)] = y;
+            })
+        } else {
+            PV_FOR_BINS(E, lane, {
+                float sn, cs;
+                sincos_pv(phc[i], &sn, &cs);
+                float2 y = make_float2(mag[i] * cs, mag[i] * sn);
+                if (k == 0 || k == L) y.y = 0.0f;
+                tile[G_::pad(k)] = y;
+            })
+        }
+    } else {
+        PV_FOR_BINS(E, lane, {
+            float sn, cs;
+            sincos_pv(ph[i], &sn, &cs);
+            const float xr = mag[i] * cs;                 // kernel.cu:127
+            float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
+            if (k == 0 || k == L) y.y = 0.0f;
+            tile[G_::pad(k)] = y;
+        })
+    }
+    wave_lds_sync();
+    // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
+    const float2* baseA = tile + G_::pad(lane);
+    const float2* baseB = tile + G_::pad(L - lane);
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        const int i = lane + 64 * q;
+        const float2 A = lds_ld(&baseA[G_::padc(64 * q)]);
+        const float2 Bc = lds_ld(&baseB[-G_::padc(64 * q)]);
+        const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
+        const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
+        const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
+        const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
+        const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
+        z[q] = make_float2(fer - Foi, fei + For);
+    }
+    wave_lds_sync();
+    fft_run<L, true, STORE_LAST>(z, tile, twl, tw0, lane);
+}
+
+}  // namespace pv

@@ -12,134 +12,10 @@
 // Geometry: one frame per wavefront, and each wave owns a RUN of F consecutive frames of
 // one channel which it walks in order (the unwrap state stays in registers, the
 // overlap-add in a per-wave LDS ring).  A workgroup = 4 waves = 4 consecutive runs.
-#include "pv_device.hpp"
+#include "pv_frame.hpp"
 #include "pv_kernels.h"
 
 namespace pv {
-
-// ------------------------------------------------------------------ shared frame code
-// Load frame t (window applied) into the pass-0 register layout: z[q] = (xw[2i], xw[2i+1]),
-// i = lane + 64 q.  Samples at index >= n read as 0.
-template <int L>
-__device__ __forceinline__ void load_frame_std(float2 (&z)[Geo<L>::E], const float* __restrict__ xc,
-                                               long long base, long long n, const float* __restrict__ win,
-                                               int aligned, int lane) {
-    constexpr int E = Geo<L>::E;
-    constexpr int N = 2 * L;
-    if (aligned && base + N <= n) {
-#pragma unroll
-        for (int q = 0; q < E; ++q) {
-            const int i = lane + 64 * q;
-            const float2 xv = *reinterpret_cast<const float2*>(xc + base + 2 * i);
-            const float2 wv = *reinterpret_cast<const float2*>(win + 2 * i);
-            z[q].x = xv.x * wv.x;
-            z[q].y = xv.y * wv.y;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < E; ++q) {
-            const int i = lane + 64 * q;
-            const long long s = base + 2 * i;
-            const float x0 = (s < n) ? xc[s] : 0.0f;
-            const float x1 = (s + 1 < n) ? xc[s + 1] : 0.0f;
-            z[q].x = x0 * win[2 * i];
-            z[q].y = x1 * win[2 * i + 1];
-        }
-    }
-}
-
-// Real-FFT split of bin k (0 <= k <= L) from the natural-order L-point transform in tile.
-template <int L>
-__device__ __forceinline__ float2 real_split(const float2* tile, const float2* __restrict__ tws, int k) {
-    using G_ = Geo<L>;
-    const float2 A = tile[G_::pad(k & (L - 1))];
-    const float2 Bz = tile[G_::pad((L - k) & (L - 1))];
-    const float er = 0.5f * (A.x + Bz.x);
-    const float ei = 0.5f * (A.y - Bz.y);
-    const float orr = 0.5f * (A.y + Bz.y);
-    const float oi = 0.5f * (Bz.x - A.x);
-    const float2 tw = tws[k];
-    float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
-    float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
-    if (k == 0 || k == L) Xi = 0.0f;
-    return make_float2(Xr, Xi);
-}
-
-// All bins of a lane at once (LDS reads batched ahead of the arithmetic).
-template <int L>
-__device__ __forceinline__ void real_split_all(const float2* tile, const float2* twsl, int lane,
-                                               float2 (&X)[Geo<L>::E + 1]) {
-    using G_ = Geo<L>;
-    constexpr int E = G_::E;
-    float2 A[E + 1], Bz[E + 1], tw[E + 1];
-#pragma unroll
-    for (int i = 0; i <= E; ++i) {
-        const int k = (i == E) ? ((lane == 0) ? L : 0) : lane + 64 * i;
-        A[i] = tile[G_::pad(k & (L - 1))];
-        Bz[i] = tile[G_::pad((L - k) & (L - 1))];
-        tw[i] = twsl[k];
-    }
-#pragma unroll
-    for (int i = 0; i <= E; ++i) {
-        const int k = (i == E) ? ((lane == 0) ? L : 0) : lane + 64 * i;
-        const float er = 0.5f * (A[i].x + Bz[i].x);
-        const float ei = 0.5f * (A[i].y - Bz[i].y);
-        const float orr = 0.5f * (A[i].y + Bz[i].y);
-        const float oi = 0.5f * (Bz[i].x - A[i].x);
-        float Xr = er + __builtin_fmaf(orr, tw[i].x, -(oi * tw[i].y));
-        float Xi = ei + __builtin_fmaf(orr, tw[i].y, oi * tw[i].x);
-        if (k == 0 || k == L) Xi = 0.0f;
-        X[i] = make_float2(Xr, Xi);
-    }
-}
-
-// Bins i0 .. i0+CH-1 of a lane (reads batched; entries past E are dummies).
-template <int L, int CH>
-__device__ __forceinline__ void split_chunk(const float2* tile, const float2* twsl, int lane, int i0,
-                                            float2 (&X)[CH]) {
-    using G_ = Geo<L>;
-    constexpr int E = G_::E;
-    // A = Z[k], B = Z[(L-k) mod L], k = lane + 64 i: affine in i from two per-lane bases;
-    // only (lane 0, i = 0) wraps (B = Z[0]) and bin L (i = E, lane 0) uses Z[0] twice.
-    const float2* baseA = tile + G_::pad(lane);
-    const float2* baseB = tile + G_::pad(L - lane);
-    const float2* baseT = twsl + lane;
-    float2 A[CH], Bz[CH], tw[CH];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        if (i < E) {
-            A[c] = lds_ld(&baseA[G_::padc(64 * i)]);
-            Bz[c] = lds_ld((i == 0 && lane == 0) ? tile : &baseB[-G_::padc(64 * i)]);
-            tw[c] = lds_ld(&baseT[64 * i]);
-        } else {
-            A[c] = lds_ld(tile);
-            Bz[c] = A[c];
-            tw[c] = lds_ld(&twsl[L]);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        const float er = 0.5f * (A[c].x + Bz[c].x);
-        const float ei = 0.5f * (A[c].y - Bz[c].y);
-        const float orr = 0.5f * (A[c].y + Bz[c].y);
-        const float oi = 0.5f * (Bz[c].x - A[c].x);
-        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
-        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
-        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
-        X[c] = make_float2(Xr, Xi);
-    }
-}
-
-// bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
-#define PV_FOR_BINS(E_, lane_, ...)                              \
-    _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \
-        if (i == (E_) && (lane_) != 0) break;                    \
-        const int k = (i == (E_)) ? 64 * (E_) : (lane_) + 64 * i; \
-        (void)k;                                                 \
-        __VA_ARGS__                                              \
-    }
 
 // ------------------------------------------------------------------ K1 STANDARD
 // One wave = one run of F consecutive frames (plus the halo frame t0-1, transformed only
@@ -175,11 +51,13 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
     float phprev[E + 1];
-    int sacc[E + 1], m0[E + 1];
-    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; m0[i] = 0; })
+    int sacc[E + 1];
+    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; })
+    // run record {S, m0}: m0 (the decision of the run's first frame) is stored as soon as
+    // it is known, S after the loop
+    int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * 2 * BP : nullptr;
 
     // One frame: window + FFT + split + atan2 (+ spectrum row, decisions) from raw samples.
-    // One frame: window + FFT + split + atan2 (+ magnitude, unwrap decisions) into res.
     // HALO (frame t0 - 1): phase only, it seeds phprev.
     auto window = [&](const float2 (&xr)[E], float2 (&z)[E]) {
         const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
@@ -214,7 +92,7 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
                     // bin L (i = E) has the same value and address on every lane
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
                     const int m = unwrap_count(ph, phprev[i], lds_ld(&ekl[k]));
-                    m0[i] = (u == 0) ? m : m0[i];
+                    if (u == 0 && rec != nullptr && (i < E || lane == 0)) rec[BP + k] = m;
                     sacc[i] += (u == 0) ? 0 : m;
                 }
                 phprev[i] = ph;
@@ -283,10 +161,7 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
         window(xr, z);
         frame(u, z, std::false_type{});
     }
-    if (p.runsum != nullptr) {
-        int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * BP;
-        PV_FOR_BINS(E, lane, { dst[k] = sacc[i]; dst[BP + k] = m0[i]; })
-    }
+    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = sacc[i]; })
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT
@@ -496,99 +371,11 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
         }
     }
 
-    // One frame t = t0 + u from its spectrum row sv (mag, phase of this lane's bins):
-    // phase processing, C2R pre-split, inverse FFT.  ROLA: result left in z (last-pass
-    // register layout); ring path: result in tile.
+    const PhaseMap pmap{p.rho, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
+    const SynLds stb{twl, twsl, ekl, jkl, srcl};
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
-        float mag[E + 1], ph[E + 1];
-        PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
-        if constexpr (MODE != 1) {
-            const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
-            float phc[E + 1];
-            float ekv[E + 1];
-            unsigned jkv[E + 1];
-            PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
-            PV_FOR_BINS(E, lane, {
-                const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
-                M[i] += (u > 0) ? mm : 0;
-                phprev[i] = ph[i];
-            })
-            // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
-            // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
-            const unsigned qq = (unsigned)p.q, pm = (unsigned)p.p_mod;
-            if (p.q_pow2) {
-                PV_FOR_BINS(E, lane, {
-                    const unsigned x = pm * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
-                    phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * p.inv_q));
-                })
-            } else {
-                PV_FOR_BINS(E, lane, {
-                    int mdq = M[i] % (int)qq;
-                    mdq += (mdq < 0) ? (int)qq : 0;
-                    const unsigned x = pm * (unsigned)mdq + tq * jkv[i];
-                    phc[i] = __builtin_fmaf(p.rho, ph[i], kTwoPi * ((float)(x % qq) * p.inv_q));
-                })
-            }
-            if constexpr (MODE == 2) {
-                float2 Y[E + 1];
-                PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
-                wave_lds_sync();
-                PV_FOR_BINS(E, lane, {
-                    const int s = srcl[k];
-                    float ms = 0.0f, pc = 0.0f;
-                    if (s >= 0) {
-                        const int cnt = srcl[B + k];
-                        pc = tile[G_::pad(s)].y;
-                        for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
-                    }
-                    float sn, cs;
-                    sincos_pv(pc, &sn, &cs);
-                    Y[i] = make_float2(ms * cs, ms * sn);
-                })
-                wave_lds_sync();
-                PV_FOR_BINS(E, lane, {
-                    float2 y = Y[i];
-                    if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
-                    tile[G_::pad(k)] = y;
-                })
-            } else {
-                PV_FOR_BINS(E, lane, {
-                    float sn, cs;
-                    sincos_pv(phc[i], &sn, &cs);
-                    float2 y = make_float2(mag[i] * cs, mag[i] * sn);
-                    if (k == 0 || k == L) y.y = 0.0f;
-                    tile[G_::pad(k)] = y;
-                })
-            }
-        } else {
-            PV_FOR_BINS(E, lane, {
-                float sn, cs;
-                sincos_pv(ph[i], &sn, &cs);
-                const float xr = mag[i] * cs;                 // kernel.cu:127
-                float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
-                if (k == 0 || k == L) y.y = 0.0f;
-                tile[G_::pad(k)] = y;
-            })
-        }
-        wave_lds_sync();
-        // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
-        const float2* baseA = tile + G_::pad(lane);
-        const float2* baseB = tile + G_::pad(L - lane);
-#pragma unroll
-        for (int q = 0; q < E; ++q) {
-            const int i = lane + 64 * q;
-            const float2 A = lds_ld(&baseA[G_::padc(64 * q)]);
-            const float2 Bc = lds_ld(&baseB[-G_::padc(64 * q)]);
-            const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
-            const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
-            const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
-            const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
-            const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
-            z[q] = make_float2(fer - Foi, fei + For);
-        }
-        wave_lds_sync();
-        if constexpr (ROLA) fft_run<L, true, false>(z, tile, twl, tw0, lane);
-        else fft_run<L, true>(z, tile, twl, tw0, lane);
+        const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
+        synth_frame<L, MODE, !ROLA>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
