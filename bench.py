@@ -95,7 +95,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--workload", choices=["batch", "rt"], default="batch",
+                    help="batch: configs[2] (default, the headline line); rt: configs[4]")
     args = ap.parse_args()
+    if args.workload == "rt":
+        return bench_rt(args)
 
     import torch
     import torch.distributed as dist
@@ -203,6 +207,71 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_rt(args):
+    """BASELINE configs[4]: real-time ring-buffer mode, 256 channels, N=256, hop=64
+    (64-sample callbacks at 44.1 kHz: 1.451 ms deadline), PV_STANDARD pitch shift 1.5,
+    one hipGraph replay per callback (pinned host in -> device -> kernel -> pinned host
+    out).  A step = one synchronous callback; latency percentiles are host wall-clock per
+    callback (what an RtAudio thread waits for)."""
+    import torch
+    from pvamd import PITCH_SHIFT, RealTimeVocoder
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(local)
+    C, N, hop_div, scale = args.channels if args.channels != 1024 else 256, 256, 4, 1.5
+    rt = RealTimeVocoder(N, PITCH_SHIFT, scale, hop_div, channels=C, device=local)
+    hop = rt.hopSize
+    steps = args.steps if args.steps != 10 else 2000
+    warm = max(args.warmup, 50)
+    rt.capture(1)
+    blocks = synth_channels_np(C, hop * 64, 20240).reshape(C, 64, hop)
+    for j in range(warm):
+        rt.host_in[:] = blocks[:, j % 64]
+        rt.callback()
+    lat = np.empty(steps)
+    t0 = time.perf_counter()
+    for j in range(steps):
+        a = time.perf_counter_ns()
+        rt.host_in[:] = blocks[:, j % 64]          # main.cpp:49 memcpy into curr_input
+        rt.callback()
+        lat[j] = (time.perf_counter_ns() - a) * 1e-3
+    dt = time.perf_counter() - t0
+    # device time of the per-callback kernel alone (events on the push stream)
+    x = torch.from_numpy(blocks[:, 0].copy()).cuda()
+    out = torch.empty((C, rt.outHopSize), device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(20):
+        rt.push(x, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(200):
+        rt.push(x, out=out)
+    e1.record(s)
+    torch.cuda.synchronize()
+    k_us = e0.elapsed_time(e1) / 200 * 1e3
+    deadline_us = hop / SR * 1e6
+    frame_bytes = 4 * hop + 4 * rt.outHopSize  # SURVEY.md §8(d) fused-mode bytes per frame
+    line = {
+        "metric": METRIC + " [real-time mode]", "value": C * steps / dt, "unit": "frames/s",
+        "n_gpus": 1, "steps": steps, "warmup": warm, "ms_per_step": dt / steps * 1e3,
+        "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (3 sines + noise), 64-sample blocks cycled",
+        "config": {"workload": "BASELINE configs[4]: real-time ring buffer, 256 ch, N=256 hop=64, "
+                               "PV_STANDARD pitch 1.5, hipGraph per callback",
+                   "channels": C, "N": N, "hop": hop, "out_hop": rt.outHopSize},
+        "latency_us": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                       "max": float(lat.max()), "deadline": deadline_us,
+                       "missed": int(np.sum(lat > deadline_us))},
+        "kernel_us": k_us,
+        "roofline": {"bound": "latency", "kernel": "rt", "achieved": C * frame_bytes / (k_us * 1e-6) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": C * frame_bytes / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None},
+        "world_size_env": world,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def pv_frames(n, hop):

@@ -20,6 +20,13 @@
  *   pv_process       analysis -> processing -> resynthesis fused pipeline (the offline
  *                      loop of main.cpp:228-297 in one call); no reference counterpart
  *   pv_frame_*       the hop/frame arithmetic of main.cpp:231 and main.cpp:266
+ *   pv_rt_*          the real-time design: RtAudio `callback` (main.cpp:45-59) copying each
+ *                      buffer into PhaseVocoder::curr_input and calling the per-callback
+ *                      PhaseVocoder::analysis() over prev_input / prev_mag_phase /
+ *                      prev_output (phaseVocoder.h:16-31; pv_analysis_RT kernel.cu:219-250;
+ *                      README.md:46-50); one hipGraph replay per callback
+ *   pv_fft_c2c       FFT::HPFFT::computeGPUFFT / computeGPUIFFT (karnel/hpfft.h:6-11,
+ *                      hpfft.cu:145-203): radix-2 Stockham FFT, batched in one launch
  *
  * Errors: status codes instead of the reference's print-and-exit (io.cpp:115-124).  The
  * header-only C++ drop-in (include/phaseVocoder.h) restores print-and-exit on top.
@@ -111,6 +118,41 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);
+
+/* ---------------------------------------------------------------- real-time mode
+ * A pv_rt streams `channels` mono channels through the STANDARD pipeline one callback at a
+ * time.  State (input history, previous phases, unwrap counts, overlap accumulator) lives
+ * on the device between calls.  A push of `nframes` frames consumes nframes*hop new
+ * samples per channel and emits nframes*out_hop final samples per channel; the emitted
+ * stream equals pv_process() of the same stream prefixed with N - hop zeros.
+ * Supported: PV_MODE_STANDARD, n_samps in [256, 2048]. */
+typedef struct pv_rt pv_rt;
+
+pv_status pv_rt_create(const pv_config* cfg, int channels, pv_rt** out);
+void pv_rt_destroy(pv_rt* rt);
+/* zero the stream state (start of a new stream) */
+pv_status pv_rt_reset(pv_rt* rt, void* stream);
+/* device pointers: in[c*ldi + i], i < nframes*hop; out[c*ldo + i], i < nframes*out_hop;
+ * spec (nullable) receives the analysed {mag, phase} rows: spec[c*ld_spec + f*spec_stride + k] */
+pv_status pv_rt_push(pv_rt* rt, const float* in, long long ldi, int nframes, float* out,
+                     long long ldo, pv_float2* spec, long long ld_spec, void* stream);
+/* Capture one callback of `nframes` frames into a hipGraph: pinned host input -> device,
+ * pv_rt_push, device -> pinned host output.  The pinned buffers are planar
+ * [channels][nframes*hop] and [channels][nframes*out_hop] (pv_rt_host_buffers). */
+pv_status pv_rt_capture(pv_rt* rt, int nframes);
+pv_status pv_rt_host_buffers(pv_rt* rt, float** host_in, float** host_out);
+/* One synchronous callback on the captured graph: copies `in` (host, planar, may be the
+ * pinned buffer itself) into the pinned input, replays the graph, waits, copies the
+ * result to `out` (host, may be the pinned output itself). */
+pv_status pv_rt_callback(pv_rt* rt, const float* in, float* out);
+
+/* ---------------------------------------------------------------- standalone FFT
+ * Batched unnormalised complex FFT (both directions, like the reference's GPU_FFT):
+ * out[b*n + k] = sum_j in[b*n + j] * exp(-+2 pi i jk/n), b < batch, n a power of two in
+ * [2, 2048]; in == out (in place) is allowed.  inverse != 0 uses exp(+...).  Device
+ * pointers on the current HIP device; the first call per (device, n) builds that size's
+ * twiddle table (allocation: not capturable), later calls are. */
+pv_status pv_fft_c2c(const pv_float2* in, pv_float2* out, int n, int batch, int inverse, void* stream);
 
 /* Constant tables of a handle (windows, gains, twiddles, unwrap tables, pitch map) as one
  * device blob, so that one rank can build them and the others receive them over RCCL

@@ -9,7 +9,10 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -34,10 +37,10 @@ pv_status fail(pv_status s, const std::string& msg) {
     } while (0)
 
 constexpr double kPi = 3.14159265358979323846;
-constexpr int kNumKernels = 6;
-const char* kKernelNames[kNumKernels] = {"analysis", "runsum", "carry",
-                                         "synthesis", "seam", "compat_analysis"};
-enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5 };
+constexpr int kNumKernels = 7;
+const char* kKernelNames[kNumKernels] = {"analysis", "runsum", "carry", "synthesis",
+                                         "seam", "compat_analysis", "rt"};
+enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5, KRT = 6 };
 
 bool is_pow2(long long v) { return v > 0 && (v & (v - 1)) == 0; }
 
@@ -539,6 +542,8 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
 }
 
+}  // extern "C"
+
 namespace {
 struct TableBlobHeader {
     uint32_t magic, version;
@@ -585,6 +590,8 @@ TableBlobHeader blob_header(const pv_handle* h) {
 }
 size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 }  // namespace
+
+extern "C" {
 
 pv_status pv_export_tables(const pv_handle* h, void* dst, size_t cap, size_t* bytes, void* stream) {
     if (!h || !bytes) return fail(PV_ERR_ARG, "null argument");
@@ -680,3 +687,252 @@ void pv_profile_reset(pv_handle* h) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- real-time mode
+// pv_rt: a pv_handle (tables) + per-channel stream state + an optional captured graph
+// of one callback (pinned host in -> device -> pv_rt_push -> pinned host out).
+struct pv_rt {
+    pv_handle* h = nullptr;
+    int channels = 0;
+    float *d_hist = nullptr, *d_ola = nullptr, *d_phprev = nullptr;
+    int* d_M = nullptr;
+    unsigned* d_tcount = nullptr;
+    // captured callback
+    int g_nframes = 0;
+    float *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    hipStream_t g_stream = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+namespace {
+void rt_release_graph(pv_rt* rt) {
+    if (rt->exec) (void)hipGraphExecDestroy(rt->exec);
+    if (rt->graph) (void)hipGraphDestroy(rt->graph);
+    if (rt->h_in) (void)hipHostFree(rt->h_in);
+    if (rt->h_out) (void)hipHostFree(rt->h_out);
+    if (rt->d_in) (void)hipFree(rt->d_in);
+    if (rt->d_out) (void)hipFree(rt->d_out);
+    rt->exec = nullptr;
+    rt->graph = nullptr;
+    rt->h_in = rt->h_out = rt->d_in = rt->d_out = nullptr;
+    rt->g_nframes = 0;
+}
+}  // namespace
+
+extern "C" {
+
+void pv_rt_destroy(pv_rt* rt) {
+    if (!rt) return;
+    if (rt->h) {
+        DeviceGuard g(rt->h->cfg.device);
+        rt_release_graph(rt);
+        if (rt->g_stream) (void)hipStreamDestroy(rt->g_stream);
+        void* ptrs[] = {rt->d_hist, rt->d_ola, rt->d_phprev, rt->d_M, rt->d_tcount};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        pv_destroy(rt->h);
+    }
+    delete rt;
+}
+
+pv_status pv_rt_reset(pv_rt* rt, void* stream) {
+    if (!rt) return fail(PV_ERR_ARG, "null rt");
+    DeviceGuard g(rt->h->cfg.device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t C = (size_t)rt->channels, N = rt->h->N, BP = rt->h->bins_pad;
+    PV_HIP(hipMemsetAsync(rt->d_hist, 0, sizeof(float) * C * N, s));
+    PV_HIP(hipMemsetAsync(rt->d_ola, 0, sizeof(float) * C * N, s));
+    PV_HIP(hipMemsetAsync(rt->d_phprev, 0, sizeof(float) * C * BP, s));
+    PV_HIP(hipMemsetAsync(rt->d_M, 0, sizeof(int) * C * BP, s));
+    PV_HIP(hipMemsetAsync(rt->d_tcount, 0, sizeof(unsigned) * C, s));
+    return PV_OK;
+}
+
+pv_status pv_rt_create(const pv_config* cfg, int channels, pv_rt** out) {
+    if (!cfg || !out) return fail(PV_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (cfg->mode != PV_MODE_STANDARD)
+        return fail(PV_ERR_UNSUPPORTED, "real-time mode runs the STANDARD pipeline only");
+    if (channels <= 0) return fail(PV_ERR_ARG, "channels must be > 0");
+    pv_config c = *cfg;
+    c.max_channels = channels;
+    c.max_frames = std::max(c.max_frames, 1);
+    pv_rt* rt = new pv_rt();
+    pv_status st = pv_create(&c, &rt->h);
+    if (st != PV_OK) {
+        delete rt;
+        return st;
+    }
+    rt->channels = channels;
+    if (pv::rt_lds_bytes(rt->h->L_syn) == 0) {
+        pv_rt_destroy(rt);
+        return fail(PV_ERR_UNSUPPORTED, "real-time mode: n_samps in [256, 2048]");
+    }
+    DeviceGuard g(cfg->device);
+    const size_t C = (size_t)channels, N = rt->h->N, BP = rt->h->bins_pad;
+    auto alloc = [&](void** p, size_t bytes) -> pv_status {
+        hipError_t e = hipMalloc(p, bytes);
+        if (e != hipSuccess) return fail(PV_ERR_NOMEM, std::string("pv_rt_create: ") + hipGetErrorString(e));
+        return PV_OK;
+    };
+    if ((st = alloc((void**)&rt->d_hist, sizeof(float) * C * N)) != PV_OK ||
+        (st = alloc((void**)&rt->d_ola, sizeof(float) * C * N)) != PV_OK ||
+        (st = alloc((void**)&rt->d_phprev, sizeof(float) * C * BP)) != PV_OK ||
+        (st = alloc((void**)&rt->d_M, sizeof(int) * C * BP)) != PV_OK ||
+        (st = alloc((void**)&rt->d_tcount, sizeof(unsigned) * C)) != PV_OK) {
+        pv_rt_destroy(rt);
+        return st;
+    }
+    if ((st = pv_rt_reset(rt, nullptr)) != PV_OK || hipDeviceSynchronize() != hipSuccess) {
+        pv_rt_destroy(rt);
+        return st != PV_OK ? st : fail(PV_ERR_HIP, "pv_rt_create: reset failed");
+    }
+    *out = rt;
+    return PV_OK;
+}
+
+pv_status pv_rt_push(pv_rt* rt, const float* in, long long ldi, int nframes, float* out,
+                     long long ldo, pv_float2* spec, long long ld_spec, void* stream) {
+    if (!rt) return fail(PV_ERR_ARG, "null rt");
+    if (nframes < 0) return fail(PV_ERR_ARG, "negative nframes");
+    if (nframes == 0) return PV_OK;
+    pv_handle* h = rt->h;
+    if (!in || !out) return fail(PV_ERR_ARG, "null in/out");
+    if (rt->channels > 1 && (ldi < (long long)nframes * h->hop || ldo < (long long)nframes * h->hs))
+        return fail(PV_ERR_ARG, "ldi/ldo smaller than one callback");
+    if (spec && rt->channels > 1 && ld_spec < (long long)nframes * h->spec_stride)
+        return fail(PV_ERR_ARG, "ld_spec < nframes * spec_stride");
+    DeviceGuard g(h->cfg.device);
+    pv::RtParams p{};
+    p.in = in;
+    p.ldi = ldi;
+    p.out = out;
+    p.ldo = ldo;
+    p.spec = reinterpret_cast<float2*>(spec);
+    p.ld_spec = ld_spec;
+    p.spec_stride = h->spec_stride;
+    p.channels = rt->channels;
+    p.nframes = nframes;
+    p.hop = h->hop;
+    p.hs = h->hs;
+    p.bins_pad = h->bins_pad;
+    p.hist = rt->d_hist;
+    p.ola = rt->d_ola;
+    p.phprev = rt->d_phprev;
+    p.M = rt->d_M;
+    p.tcount = rt->d_tcount;
+    p.win = h->d_win;
+    p.gain = h->d_gain;
+    p.tw = h->d_tw_syn;
+    p.tws = h->d_tws_syn;
+    p.ek = h->d_ek;
+    p.jk_mod = h->d_jk_mod;
+    p.src_first = h->d_src_first;
+    p.src_cnt = h->d_src_cnt;
+    p.rho = h->rho;
+    p.p_mod = h->p_mod;
+    p.q = h->q;
+    p.q_pow2 = h->q_pow2;
+    p.inv_q = h->inv_q;
+    hipStream_t s = (hipStream_t)stream;
+    PV_LAUNCH(h, KRT, s, pv::launch_rt(h->L_syn, h->pitch ? 2 : 0, p, s));
+    return PV_OK;
+}
+
+pv_status pv_rt_capture(pv_rt* rt, int nframes) {
+    if (!rt) return fail(PV_ERR_ARG, "null rt");
+    if (nframes <= 0) return fail(PV_ERR_ARG, "nframes must be > 0");
+    pv_handle* h = rt->h;
+    DeviceGuard g(h->cfg.device);
+    rt_release_graph(rt);
+    if (!rt->g_stream) PV_HIP(hipStreamCreateWithFlags(&rt->g_stream, hipStreamNonBlocking));
+    const size_t C = (size_t)rt->channels;
+    const size_t ni = (size_t)nframes * h->hop, no = (size_t)nframes * h->hs;
+    PV_HIP(hipHostMalloc((void**)&rt->h_in, sizeof(float) * C * ni, hipHostMallocDefault));
+    PV_HIP(hipHostMalloc((void**)&rt->h_out, sizeof(float) * C * no, hipHostMallocDefault));
+    PV_HIP(hipMalloc((void**)&rt->d_in, sizeof(float) * C * ni));
+    PV_HIP(hipMalloc((void**)&rt->d_out, sizeof(float) * C * no));
+    std::memset(rt->h_in, 0, sizeof(float) * C * ni);
+    std::memset(rt->h_out, 0, sizeof(float) * C * no);
+    const bool was_prof = h->prof.enabled;
+    h->prof.enabled = false;  // no event records inside the graph
+    hipStream_t s = rt->g_stream;
+    PV_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    pv_status st = PV_OK;
+    if (hipMemcpyAsync(rt->d_in, rt->h_in, sizeof(float) * C * ni, hipMemcpyHostToDevice, s) != hipSuccess)
+        st = fail(PV_ERR_HIP, "pv_rt_capture: H2D capture failed");
+    if (st == PV_OK)
+        st = pv_rt_push(rt, rt->d_in, (long long)ni, nframes, rt->d_out, (long long)no, nullptr, 0, s);
+    if (st == PV_OK &&
+        hipMemcpyAsync(rt->h_out, rt->d_out, sizeof(float) * C * no, hipMemcpyDeviceToHost, s) != hipSuccess)
+        st = fail(PV_ERR_HIP, "pv_rt_capture: D2H capture failed");
+    hipGraph_t graph = nullptr;
+    hipError_t e = hipStreamEndCapture(s, &graph);
+    h->prof.enabled = was_prof;
+    if (st != PV_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return st;
+    }
+    if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    rt->graph = graph;
+    PV_HIP(hipGraphInstantiate(&rt->exec, graph, nullptr, nullptr, 0));
+    rt->g_nframes = nframes;
+    return PV_OK;
+}
+
+pv_status pv_rt_host_buffers(pv_rt* rt, float** host_in, float** host_out) {
+    if (!rt || !rt->exec) return fail(PV_ERR_ARG, "no captured callback (pv_rt_capture)");
+    if (host_in) *host_in = rt->h_in;
+    if (host_out) *host_out = rt->h_out;
+    return PV_OK;
+}
+
+pv_status pv_rt_callback(pv_rt* rt, const float* in, float* out) {
+    if (!rt || !rt->exec) return fail(PV_ERR_ARG, "no captured callback (pv_rt_capture)");
+    pv_handle* h = rt->h;
+    DeviceGuard g(h->cfg.device);
+    const size_t C = (size_t)rt->channels;
+    const size_t ni = (size_t)rt->g_nframes * h->hop, no = (size_t)rt->g_nframes * h->hs;
+    if (in && in != rt->h_in) std::memcpy(rt->h_in, in, sizeof(float) * C * ni);  // main.cpp:49
+    PV_HIP(hipGraphLaunch(rt->exec, rt->g_stream));
+    PV_HIP(hipStreamSynchronize(rt->g_stream));
+    if (out && out != rt->h_out) std::memcpy(out, rt->h_out, sizeof(float) * C * no);
+    return PV_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- standalone FFT
+namespace {
+std::mutex g_fft_mu;
+std::map<std::pair<int, int>, float2*> g_fft_tw;  // (device, n) -> stage-major twiddles
+}  // namespace
+
+extern "C" pv_status pv_fft_c2c(const pv_float2* in, pv_float2* out, int n, int batch, int inverse,
+                                void* stream) {
+    if (!in || !out) return fail(PV_ERR_ARG, "null in/out");
+    if (batch < 0) return fail(PV_ERR_ARG, "negative batch");
+    if (!is_pow2(n) || n < 2 || n > 2048) return fail(PV_ERR_UNSUPPORTED, "fft size: power of two in [2, 2048]");
+    if (batch == 0) return PV_OK;
+    int dev = 0;
+    PV_HIP(hipGetDevice(&dev));
+    float2* tw = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_fft_mu);
+        auto it = g_fft_tw.find({dev, n});
+        if (it == g_fft_tw.end()) {
+            std::vector<float2> t;
+            stage_twiddles(n, t);
+            pv_status st = upload(&tw, t);
+            if (st != PV_OK) return st;
+            g_fft_tw[{dev, n}] = tw;
+        } else {
+            tw = it->second;
+        }
+    }
+    hipError_t e = pv::launch_fft(n, inverse ? 1 : 0, reinterpret_cast<const float2*>(in),
+                                  reinterpret_cast<float2*>(out), tw, batch, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("fft launch: ") + hipGetErrorString(e));
+    return PV_OK;
+}

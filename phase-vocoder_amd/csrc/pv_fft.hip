@@ -1,0 +1,104 @@
+// pv_fft.hip — the standalone batched complex FFT op: the
+// reference's hand-written radix-2 Stockham FFT, FFT::HPFFT::computeGPUFFT /
+// computeGPUIFFT (karnel/hpfft.h:6-11, hpfft.cu:145-203), one launch for a whole batch.
+//
+// The reference runs log2(N) single-block launches per transform (GPU_FFT, one radix-2
+// stage each, ping-ponging through global memory).  Here:
+//   N in [128, 2048]: one transform per wavefront, the register-blocked Stockham engine of
+//     the phase-vocoder kernels (fft_run, pv_device.hpp): the same radix-2 butterflies
+//     with table twiddles, log2(N/64) stages per register pass, an LDS exchange per pass.
+//   N in [2, 64]: one transform per wavefront, lanes hold points, one radix-2 stage per
+//     LDS round (the reference's FftIteration, in LDS instead of global memory).
+// Unnormalised in both directions, like the reference (GPU_FFT applies no 1/N).
+#include "pv_device.hpp"
+#include "pv_kernels.h"
+
+namespace pv {
+
+template <int L, bool INV>
+__global__ __launch_bounds__(256) void k_fft(const float2* __restrict__ in, float2* out,
+                                              const float2* __restrict__ tw, int batch) {
+    using G_ = Geo<L>;
+    constexpr int E = G_::E;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2* twl = reinterpret_cast<float2*>(smem);
+    float2* tiles = twl + L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float2 tw0[E];
+    load_tw0<L>(tw0, tw);
+    for (int i = tid; i < L; i += 256) twl[i] = tw[i];
+    __syncthreads();
+    const long long b = (long long)blockIdx.x * 4 + w;
+    if (b >= batch) return;
+    float2* tile = tiles + w * G_::TILE;
+    const float2* src = in + b * L + lane;
+    float2 z[E];
+#pragma unroll
+    for (int q = 0; q < E; ++q) z[q] = src[64 * q];
+    fft_run<L, INV>(z, tile, twl, tw0, lane);
+    // all loads of this transform precede every store: in-place (in == out) is safe
+    float2* dst = out + b * L + lane;
+#pragma unroll
+    for (int q = 0; q < E; ++q) dst[64 * q] = lds_ld(&tile[G_::pad(lane + 64 * q)]);
+}
+
+// N <= 64: lanes j < N/2 run butterfly j of each radix-2 Stockham stage (hpfft.cu:145-167):
+// v0 = x[j], v1 = x[j + N/2] * W(j mod Ns, Ns); y[expand(j,Ns,2)] = v0 + v1,
+// y[expand(j,Ns,2) + Ns] = v0 - v1.  Twiddle W(m, Ns) = stage-major table entry Ns-1+m.
+template <bool INV>
+__global__ __launch_bounds__(256) void k_fft_small(const float2* __restrict__ in, float2* out,
+                                                    const float2* __restrict__ tw, int n, int batch) {
+    __shared__ float2 buf[4][2][64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const long long b = (long long)blockIdx.x * 4 + w;
+    if (b >= batch) return;
+    float2* x = buf[w][0];
+    float2* y = buf[w][1];
+    if (lane < n) x[lane] = in[b * n + lane];
+    wave_lds_sync();
+    const int h = n >> 1;
+    for (int Ns = 1; Ns < n; Ns <<= 1) {
+        if (lane < h) {
+            const float2 v0 = x[lane];
+            float2 v1 = x[lane + h];
+            const int m = lane & (Ns - 1);
+            float2 t = tw[Ns - 1 + m];
+            if (INV) t.y = -t.y;
+            v1 = cmul(v1, t);
+            const int d = (lane / Ns) * 2 * Ns + m;  // expand(j, Ns, 2)
+            y[d] = make_float2(v0.x + v1.x, v0.y + v1.y);
+            y[d + Ns] = make_float2(v0.x - v1.x, v0.y - v1.y);
+        }
+        wave_lds_sync();
+        float2* t2 = x;
+        x = y;
+        y = t2;
+    }
+    if (lane < n) out[b * n + lane] = x[lane];
+}
+
+hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
+                      hipStream_t s) {
+    const dim3 grid((unsigned)((batch + 3) / 4)), block(256);
+#define PV_FFT_L(LL_)                                                                             \
+    {                                                                                             \
+        const size_t lds = sizeof(float2) * (LL_ + 4 * Geo<LL_>::TILE);                           \
+        if (inverse) hipLaunchKernelGGL((k_fft<LL_, true>), grid, block, lds, s, in, out, tw, batch); \
+        else hipLaunchKernelGGL((k_fft<LL_, false>), grid, block, lds, s, in, out, tw, batch);     \
+    }
+    switch (n) {
+        case 128: PV_FFT_L(128); break;
+        case 256: PV_FFT_L(256); break;
+        case 512: PV_FFT_L(512); break;
+        case 1024: PV_FFT_L(1024); break;
+        case 2048: PV_FFT_L(2048); break;
+        default:
+            if (n < 2 || n > 64 || (n & (n - 1))) return hipErrorInvalidValue;
+            if (inverse) hipLaunchKernelGGL((k_fft_small<true>), grid, block, 0, s, in, out, tw, n, batch);
+            else hipLaunchKernelGGL((k_fft_small<false>), grid, block, 0, s, in, out, tw, n, batch);
+    }
+#undef PV_FFT_L
+    return hipGetLastError();
+}
+
+}  // namespace pv

@@ -66,6 +66,35 @@ struct SeamParams {
     int nruns, nwg, F, hs, tail_len;
 };
 
+// real-time mode (pv_rt.hip): one launch per callback, a wave per channel
+struct RtParams {
+    const float* in;                   // [C][nframes * hop] new samples (row stride ldi)
+    long long ldi;
+    float* out;                        // [C][nframes * hs] emitted samples (row stride ldo)
+    long long ldo;
+    float2* spec;                      // optional [C][nframes][spec_stride] {mag, phase}
+    long long ld_spec;
+    int spec_stride;
+    int channels, nframes, hop, hs, bins_pad;
+    float* hist;                       // [C][N] stream state (see pv_rt.hip)
+    float* ola;                        // [C][N]
+    float* phprev;                     // [C][bins_pad]
+    int* M;                            // [C][bins_pad]
+    unsigned* tcount;                  // [C]
+    const float* win;
+    const float* gain;
+    const float2* tw;
+    const float2* tws;
+    const float* ek;
+    const unsigned* jk_mod;
+    const int* src_first;
+    const int* src_cnt;
+    float rho;
+    unsigned long long p_mod, q;
+    int q_pow2;
+    float inv_q;
+};
+
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
@@ -73,6 +102,10 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
 size_t synthesis_lds_bytes(int L, int hs);
+hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
+                      hipStream_t s);
+hipError_t launch_rt(int L, int mode, const RtParams& p, hipStream_t s);
+size_t rt_lds_bytes(int L);
 hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,
                                int n, int hop, hipStream_t s);
 

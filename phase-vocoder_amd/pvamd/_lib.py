@@ -86,6 +86,23 @@ def lib():
     L.pv_profile_read.restype = i
     L.pv_profile_reset.argtypes = [vp]
     L.pv_profile_reset.restype = None
+    L.pv_rt_create.argtypes = [ctypes.POINTER(pv_config), i, ctypes.POINTER(vp)]
+    L.pv_rt_create.restype = i
+    L.pv_rt_destroy.argtypes = [vp]
+    L.pv_rt_destroy.restype = None
+    L.pv_rt_reset.argtypes = [vp, vp]
+    L.pv_rt_reset.restype = i
+    L.pv_rt_push.argtypes = [vp, vp, ll, i, vp, ll, vp, ll, vp]
+    L.pv_rt_push.restype = i
+    L.pv_rt_capture.argtypes = [vp, i]
+    L.pv_rt_capture.restype = i
+    fpp = ctypes.POINTER(ctypes.POINTER(ctypes.c_float))
+    L.pv_rt_host_buffers.argtypes = [vp, fpp, fpp]
+    L.pv_rt_host_buffers.restype = i
+    L.pv_rt_callback.argtypes = [vp, vp, vp]
+    L.pv_rt_callback.restype = i
+    L.pv_fft_c2c.argtypes = [vp, vp, i, i, i, vp]
+    L.pv_fft_c2c.restype = i
     _lib = L
     return L
 

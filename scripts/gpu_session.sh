@@ -13,7 +13,15 @@ for step in $STEPS; do
     tests)
       timeout -k 10 "${T_TESTS:-600}" python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
-      if fatal $rc; then echo "FATAL in tests"; exit $rc; fi ;;
+      if fatal $rc || [ $rc -gt 1 ]; then echo "FATAL in tests"; exit $rc; fi ;;
+    rt)
+      timeout -k 10 "${T_BENCH:-300}" python bench.py --workload rt > gpurun_out/bench_rt.log 2>&1
+      rc=$?; echo "bench rt rc=$rc"; tail -3 gpurun_out/bench_rt.log
+      if [ $rc -ne 0 ]; then echo "bench rt failed"; exit $rc; fi ;;
+    fft)
+      timeout -k 10 120 phase-vocoder_amd/build/fft_bench bench > gpurun_out/fft_bench.log 2>&1
+      rc=$?; echo "fft bench rc=$rc"; cat gpurun_out/fft_bench.log
+      if [ $rc -ne 0 ]; then exit $rc; fi ;;
     bench)
       timeout -k 10 "${T_BENCH:-600}" python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
