@@ -161,6 +161,21 @@ __device__ __forceinline__ void sincos_pv(float x, float* sn, float* cs) {
     *cs = ((q + 1) & 2) ? -cv : cv;
 }
 
+// sin/cos of 2 pi rev.  Default: the hardware v_sin_f32 / v_cos_f32 (inputs in
+// revolutions, quarter-rate transcendental) after an exact reduction to [-1/2, 1/2]
+// (rev - rint(rev) is exact for |rev| < 2^23); PV_SOFT_SINCOS selects the polynomial
+// sincos_pv.  Synthesis parity is tolerance based, so either is in
+// contract; the GPU tests bound the end-to-end error.
+__device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
+    const float r = rev - __builtin_rintf(rev);
+#ifdef PV_SOFT_SINCOS
+    sincos_pv(r * kTwoPi, sn, cs);
+#else
+    *sn = __builtin_amdgcn_sinf(r);
+    *cs = __builtin_amdgcn_cosf(r);
+#endif
+}
+
 // unwrap decision of the contract (oracle pvr_unwrap_count)
 __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) {
     float d = (phi - phi_prev) - e;

@@ -23,7 +23,8 @@ __global__ __launch_bounds__(256) void k_fft(const float2* __restrict__ in, floa
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* twl = reinterpret_cast<float2*>(smem);
     float2* tiles = twl + L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[E];
     load_tw0<L>(tw0, tw);
     for (int i = tid; i < L; i += 256) twl[i] = tw[i];
@@ -49,7 +50,8 @@ template <bool INV>
 __global__ __launch_bounds__(256) void k_fft_small(const float2* __restrict__ in, float2* out,
                                                     const float2* __restrict__ tw, int n, int batch) {
     __shared__ float2 buf[4][2][64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     const long long b = (long long)blockIdx.x * 4 + w;
     if (b >= batch) return;
     float2* x = buf[w][0];

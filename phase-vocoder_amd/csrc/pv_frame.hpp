@@ -76,7 +76,7 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
 // STANDARD phase propagation constants: phi_s = rho phi + 2 pi ((p M_tot) mod q) / q,
 // M_tot = M_dec + (t+1) j_k
 struct PhaseMap {
-    float rho;
+    float rho_rev;  // rho / (2 pi): output phases are carried in revolutions
     unsigned q, p_mod;
     int q_pow2;
     float inv_q;
@@ -97,7 +97,9 @@ struct SynLds {
 // already holds), MODE 1 REF_COMPAT (kernel.cu:121-129 y-bug).  tq = (t + 1) mod q.
 // Result: STORE_LAST: time samples in tile (natural order, padded); else the inverse
 // FFT's last-pass registers z (point lane + 64 last_slot(idx)).
-template <int L, int MODE, bool STORE_LAST>
+// QPOW2: the output-phase denominator q is a power of two <= 2^24 (compile-time path);
+// otherwise the generic path handles any q the handle accepts.
+template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
@@ -124,20 +126,27 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             M[i] += add_decision ? mm : 0;
             phprev[i] = ph[i];
         })
-        // (p * M_tot) mod q, M_tot = M_dec + (t+1) j_k: q = 2^e -> wrapping 32-bit
-        // arithmetic is exact mod q; otherwise q <= 32768 and nothing wraps.
+        // output phase in revolutions: rho phi / 2 pi + ((p M_tot) mod q) / q,
+        // M_tot = M_dec + (t+1) j_k.  q = 2^e: wrapping 32-bit arithmetic is exact mod q
+        // (24-bit multiplies while q <= 2^24, the operands are < q); otherwise
+        // q <= 32768 and nothing wraps.
         const unsigned qq = pm.q, pmod = pm.p_mod;
-        if (pm.q_pow2) {
+        if (QPOW2) {
+            PV_FOR_BINS(E, lane, {
+                const unsigned x = __umul24(pmod, (unsigned)M[i] & (qq - 1u)) + __umul24(tq, jkv[i]);
+                phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], (float)(x & (qq - 1u)) * pm.inv_q);
+            })
+        } else if (pm.q_pow2) {
             PV_FOR_BINS(E, lane, {
                 const unsigned x = pmod * ((unsigned)M[i] & (qq - 1u)) + tq * jkv[i];
-                phc[i] = __builtin_fmaf(pm.rho, ph[i], kTwoPi * ((float)(x & (qq - 1u)) * pm.inv_q));
+                phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], (float)(x & (qq - 1u)) * pm.inv_q);
             })
         } else {
             PV_FOR_BINS(E, lane, {
                 int mdq = M[i] % (int)qq;
                 mdq += (mdq < 0) ? (int)qq : 0;
                 const unsigned x = pmod * (unsigned)mdq + tq * jkv[i];
-                phc[i] = __builtin_fmaf(pm.rho, ph[i], kTwoPi * ((float)(x % qq) * pm.inv_q));
+                phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], (float)(x % qq) * pm.inv_q);
             })
         }
         if constexpr (MODE == 2) {
@@ -153,7 +162,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                     for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
                 }
                 float sn, cs;
-                sincos_pv(pc, &sn, &cs);
+                sincos_rev(pc, &sn, &cs);
                 Y[i] = make_float2(ms * cs, ms * sn);
             })
             wave_lds_sync();
@@ -165,7 +174,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         } else {
             PV_FOR_BINS(E, lane, {
                 float sn, cs;
-                sincos_pv(phc[i], &sn, &cs);
+                sincos_rev(phc[i], &sn, &cs);
                 float2 y = make_float2(mag[i] * cs, mag[i] * sn);
                 if (k == 0 || k == L) y.y = 0.0f;
                 tile[G_::pad(k)] = y;
@@ -174,7 +183,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     } else {
         PV_FOR_BINS(E, lane, {
             float sn, cs;
-            sincos_pv(ph[i], &sn, &cs);
+            sincos_rev(ph[i] * kInv2Pi, &sn, &cs);
             const float xr = mag[i] * cs;                 // kernel.cu:127
             float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
             if (k == 0 || k == L) y.y = 0.0f;

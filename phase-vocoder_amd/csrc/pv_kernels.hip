@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
     float* ekl = winl + N;                            // B
     const int BP = p.bins_pad;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
@@ -177,7 +178,8 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     float2* twl = reinterpret_cast<float2*>(smem);
     float2* tiles = twl + L;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(256) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
-template <int L, int MODE, int DT>
+template <int L, int MODE, int DT, bool QPOW2 = false>
 __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
@@ -322,7 +324,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
     const int hs = p.hs;
     const int TL = N - hs;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) { twl[i] = p.tw[i]; twsl[i] = p.tws[i]; }
@@ -371,11 +374,12 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
         }
     }
 
-    const PhaseMap pmap{p.rho, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
+    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
+    const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
-        const unsigned tq = (unsigned)((unsigned long long)(t + 1) % p.q);
-        synth_frame<L, MODE, !ROLA>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
+        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
+        synth_frame<L, MODE, !ROLA, QPOW2>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
@@ -629,34 +633,52 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int MODE>
+// QPOW2 kernels (q a power of two <= 2^24: every STANDARD configuration with a power-of-two
+// hop) for all overlap-add variants; the generic-q path uses the LDS ring (DT = 0).
+template <int MODE, bool QP>
 static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParams& p, hipStream_t s) {
-#define PV_SYN_DT(LL_)                                                                         \
-    switch (dt) {                                                                              \
-        case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
-        case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
-        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
-        default: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0>), grid, dim3(256), syn_lds<LL_>(0), s, p); break; \
+#define PV_SYN_DT(LL_)                                                                                    \
+    switch (dt) {                                                                                         \
+        case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1, QP>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
+        case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2, QP>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
+        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
+        default: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0, QP>), grid, dim3(256), syn_lds<LL_>(0), s, p); break; \
     }
-    switch (L) {
-        case 128: PV_SYN_DT(128); break;
-        case 256: PV_SYN_DT(256); break;
-        case 512: PV_SYN_DT(512); break;
-        case 1024: PV_SYN_DT(1024); break;
-        case 2048: hipLaunchKernelGGL((k_synthesis<2048, MODE, 0>), grid, dim3(256), syn_lds<2048>(0), s, p); break;
-        default: return hipErrorInvalidValue;
+#define PV_SYN_DT0(LL_) hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0, QP>), grid, dim3(256), syn_lds<LL_>(0), s, p)
+    if constexpr (QP || MODE == 1) {
+        switch (L) {
+            case 128: PV_SYN_DT(128); break;
+            case 256: PV_SYN_DT(256); break;
+            case 512: PV_SYN_DT(512); break;
+            case 1024: PV_SYN_DT(1024); break;
+            case 2048: PV_SYN_DT0(2048); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (L) {
+            case 128: PV_SYN_DT0(128); break;
+            case 256: PV_SYN_DT0(256); break;
+            case 512: PV_SYN_DT0(512); break;
+            case 1024: PV_SYN_DT0(1024); break;
+            case 2048: PV_SYN_DT0(2048); break;
+            default: return hipErrorInvalidValue;
+        }
     }
 #undef PV_SYN_DT
+#undef PV_SYN_DT0
     return hipGetLastError();
 }
 
 // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
-    const int dt = syn_dt(L, p.hs);
-    if (mode == 0) return launch_synthesis_mode<0>(L, dt, grid, p, s);
-    if (mode == 2) return launch_synthesis_mode<2>(L, dt, grid, p, s);
-    return launch_synthesis_mode<1>(L, dt, grid, p, s);
+    const bool qp = p.q_pow2 && p.q <= (1ull << 24);
+    const int dt = (mode == 1 || qp) ? syn_dt(L, p.hs) : 0;
+    if (mode == 0) return qp ? launch_synthesis_mode<0, true>(L, dt, grid, p, s)
+                             : launch_synthesis_mode<0, false>(L, dt, grid, p, s);
+    if (mode == 2) return qp ? launch_synthesis_mode<2, true>(L, dt, grid, p, s)
+                             : launch_synthesis_mode<2, false>(L, dt, grid, p, s);
+    return launch_synthesis_mode<1, false>(L, dt, grid, p, s);
 }
 
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s) {

@@ -43,7 +43,7 @@ struct RtGeo {
     static constexpr size_t BYTES = sizeof(float) * FLOATS;
 };
 
-template <int L, int MODE>
+template <int L, int MODE, bool QPOW2>
 __global__ __launch_bounds__(256) void k_rt(RtParams p) {
     using G_ = Geo<L>;
     using R_ = RtGeo<L>;
@@ -61,7 +61,8 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
     unsigned* jkl = reinterpret_cast<unsigned*>(rsm + R_::O_JK);
     int* srcl = reinterpret_cast<int*>(rsm + R_::O_SRC);
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 64 * W) twl[i] = p.tw[i];
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
         PV_FOR_BINS(E, lane, { M[i] = Mg[k]; phprev[i] = Pg[k]; })
     }
     unsigned t = p.tcount[c];
-    const PhaseMap pmap{p.rho, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
+    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
     const float* inc = p.in + (long long)c * p.ldi;
     float* outc = p.out + (long long)c * p.ldo;
@@ -138,8 +139,9 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
         }
         wave_lds_sync();
         // ---- processing + resynthesis: time samples to tile (natural order)
-        const unsigned tq = (unsigned)(((unsigned long long)t + 1ull) % p.q);
-        synth_frame<L, MODE, true>(sv, true, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
+        const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
+        const unsigned tq = QPOW2 ? ((t + 1u) & (q32 - 1u)) : ((t + 1u) % q32);
+        synth_frame<L, MODE, true, QPOW2>(sv, true, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
         // ---- overlap-add, emit the out hop, shift
         const float* ty = reinterpret_cast<const float*>(tile);
         float nv[SPW];
@@ -200,9 +202,12 @@ int rt_waves_per_group(int L) { return L <= 512 ? 4 : 2; }
 hipError_t launch_rt(int L, int mode, const RtParams& p, hipStream_t s) {
     const int W = rt_waves_per_group(L);
     dim3 grid((p.channels + W - 1) / W), block(64 * W);
+    const bool qp = p.q_pow2 && p.q <= (1ull << 24);
 #define PV_RT_L(LL_)                                                                              \
-    if (mode == 2) hipLaunchKernelGGL((k_rt<LL_, 2>), grid, block, RtGeo<LL_>::BYTES, s, p);      \
-    else hipLaunchKernelGGL((k_rt<LL_, 0>), grid, block, RtGeo<LL_>::BYTES, s, p);
+    if (mode == 2 && qp) hipLaunchKernelGGL((k_rt<LL_, 2, true>), grid, block, RtGeo<LL_>::BYTES, s, p); \
+    else if (mode == 2) hipLaunchKernelGGL((k_rt<LL_, 2, false>), grid, block, RtGeo<LL_>::BYTES, s, p); \
+    else if (qp) hipLaunchKernelGGL((k_rt<LL_, 0, true>), grid, block, RtGeo<LL_>::BYTES, s, p);   \
+    else hipLaunchKernelGGL((k_rt<LL_, 0, false>), grid, block, RtGeo<LL_>::BYTES, s, p);
     switch (L) {
         case 128: PV_RT_L(128); break;
         case 256: PV_RT_L(256); break;
