@@ -25,6 +25,8 @@
  *                      PhaseVocoder::analysis() over prev_input / prev_mag_phase /
  *                      prev_output (phaseVocoder.h:16-31; pv_analysis_RT kernel.cu:219-250;
  *                      README.md:46-50); one hipGraph replay per callback
+ *   pv_harmon*       the harmoniser the README plans ("multiple pitch shifts on a single
+ *                      input", README.md:50): one analysis, K pitch-shift resyntheses
  *   pv_fft_c2c       FFT::HPFFT::computeGPUFFT / computeGPUIFFT (karnel/hpfft.h:6-11,
  *                      hpfft.cu:145-203): radix-2 Stockham FFT, batched in one launch
  *
@@ -145,6 +147,20 @@ pv_status pv_rt_host_buffers(pv_rt* rt, float** host_in, float** host_out);
  * pinned buffer itself) into the pinned input, replays the graph, waits, copies the
  * result to `out` (host, may be the pinned output itself). */
 pv_status pv_rt_callback(pv_rt* rt, const float* in, float* out);
+
+/* ---------------------------------------------------------------- harmoniser
+ * K voices, voice k = PITCH_SHIFT by ratios[k] of the same input, all from ONE analysis
+ * and one unwrap scan (cfg: STANDARD; effect and scale are ignored).  voices_out[k*ld_voice
+ * + c*ldo + i], i < pv_output_length (every voice has out_hop = hop); each voice equals
+ * pv_process() with its ratio.  mix (nullable): mix[c*ld_mix + i] = sum_k gains[k] * voice
+ * k (gains: host array of K floats).  At most 64 voices. */
+typedef struct pv_harmonizer pv_harmonizer;
+pv_status pv_harmonizer_create(const pv_config* cfg, const float* ratios, int voices, pv_harmonizer** out);
+void pv_harmonizer_destroy(pv_harmonizer* hz);
+pv_status pv_harmonize(pv_harmonizer* hz, const float* x, long long ldx, long long n_samples,
+                       int channels, int frames, pv_float2* spec, long long ld_spec, float* voices_out,
+                       long long ldo, long long ld_voice, const float* gains, float* mix,
+                       long long ld_mix, void* stream);
 
 /* ---------------------------------------------------------------- standalone FFT
  * Batched unnormalised complex FFT (both directions, like the reference's GPU_FFT):

@@ -200,9 +200,11 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     return PV_OK;
 }
 
+// carry_from: unwrap carries already scanned by another handle of the same analysis
+// geometry (the harmoniser's voices share one scan); nullptr = scan here.
 pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int C, int frames,
                          const float* ola_in, long long ld_ola, float* out, long long ldo,
-                         bool have_runsum, hipStream_t s) {
+                         bool have_runsum, hipStream_t s, const int* carry_from = nullptr) {
     if (C == 0 || frames == 0) {
         return PV_OK;
     }
@@ -213,7 +215,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
         return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
     const int nruns = nruns_of(h, frames);
     const float2* sp = reinterpret_cast<const float2*>(spec);
-    if (h->mode == PV_MODE_STANDARD) {
+    if (h->mode == PV_MODE_STANDARD && carry_from == nullptr) {
         pv::ScanParams sc{};
         sc.spec = sp;
         sc.ld_spec = ld_spec;
@@ -237,7 +239,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.F = h->F;
     p.nruns = nruns;
     p.bins_pad = h->bins_pad;
-    p.carry = h->d_carry;
+    p.carry = carry_from ? carry_from : h->d_carry;
     p.ek = h->d_ek;
     p.jk_mod = h->d_jk_mod;
     p.src_first = h->d_src_first;
@@ -936,3 +938,86 @@ extern "C" pv_status pv_fft_c2c(const pv_float2* in, pv_float2* out, int n, int 
     if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("fft launch: ") + hipGetErrorString(e));
     return PV_OK;
 }
+
+// ---------------------------------------------------------------- harmoniser
+// README.md:50 "harmonization of input signals (i.e. multiple pitch shifts on a single
+// input)": one analysis + one unwrap scan, then one synthesis per voice (its own pitch
+// map and output-phase ratio), optionally mixed.
+struct pv_harmonizer {
+    std::vector<pv_handle*> voices;
+};
+
+extern "C" {
+
+void pv_harmonizer_destroy(pv_harmonizer* hz) {
+    if (!hz) return;
+    for (pv_handle* v : hz->voices) pv_destroy(v);
+    delete hz;
+}
+
+pv_status pv_harmonizer_create(const pv_config* cfg, const float* ratios, int voices, pv_harmonizer** out) {
+    if (!cfg || !ratios || !out) return fail(PV_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (voices <= 0 || voices > 64) return fail(PV_ERR_ARG, "voices must be in [1, 64]");
+    if (cfg->mode != PV_MODE_STANDARD) return fail(PV_ERR_UNSUPPORTED, "the harmoniser runs the STANDARD pipeline");
+    pv_harmonizer* hz = new pv_harmonizer();
+    for (int k = 0; k < voices; ++k) {
+        pv_config c = *cfg;
+        c.effect = PV_PITCH_SHIFT;
+        c.scale = ratios[k];
+        pv_handle* h = nullptr;
+        pv_status st = pv_create(&c, &h);
+        if (st != PV_OK) {
+            pv_harmonizer_destroy(hz);
+            return st;
+        }
+        hz->voices.push_back(h);
+    }
+    *out = hz;
+    return PV_OK;
+}
+
+pv_status pv_harmonize(pv_harmonizer* hz, const float* x, long long ldx, long long n_samples,
+                       int channels, int frames, pv_float2* spec, long long ld_spec, float* voices_out,
+                       long long ldo, long long ld_voice, const float* gains, float* mix,
+                       long long ld_mix, void* stream) {
+    if (!hz || hz->voices.empty()) return fail(PV_ERR_ARG, "null harmoniser");
+    pv_handle* h0 = hz->voices[0];
+    pv_status st = check_common(h0, channels, frames);
+    if (st != PV_OK) return st;
+    if (!voices_out) return fail(PV_ERR_ARG, "null voices_out");
+    const int K = (int)hz->voices.size();
+    const long long olen = pv_output_length(h0, frames);
+    if (K > 1 && ld_voice < (long long)(channels - 1) * ldo + olen)
+        return fail(PV_ERR_ARG, "ld_voice smaller than one voice's output block");
+    if (mix && !gains) return fail(PV_ERR_ARG, "mix needs gains");
+    DeviceGuard g(h0->cfg.device);
+    hipStream_t s = (hipStream_t)stream;
+    st = do_analysis(h0, x, ldx, n_samples, channels, frames, spec, ld_spec, true, s);
+    if (st != PV_OK) return st;
+    st = do_resynthesis(h0, spec, ld_spec, channels, frames, nullptr, 0, voices_out, ldo, true, s);
+    if (st != PV_OK) return st;
+    for (int k = 1; k < K; ++k) {
+        st = do_resynthesis(hz->voices[k], spec, ld_spec, channels, frames, nullptr, 0,
+                            voices_out + (long long)k * ld_voice, ldo, true, s, h0->d_carry);
+        if (st != PV_OK) return st;
+    }
+    if (mix && channels > 0 && frames > 0) {
+        if (K > 64) return fail(PV_ERR_ARG, "too many voices to mix");
+        pv::MixParams mp{};
+        mp.src = voices_out;
+        mp.ldo = ldo;
+        mp.ld_voice = ld_voice;
+        mp.voices = K;
+        for (int k = 0; k < K; ++k) mp.gain[k] = gains[k];
+        mp.dst = mix;
+        mp.ld_mix = ld_mix;
+        mp.len = olen;
+        mp.channels = channels;
+        hipError_t e = pv::launch_mix(mp, s);
+        if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("mix launch: ") + hipGetErrorString(e));
+    }
+    return PV_OK;
+}
+
+}  // extern "C"

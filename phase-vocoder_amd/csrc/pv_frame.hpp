@@ -5,6 +5,13 @@
 #pragma once
 #include "pv_device.hpp"
 
+#ifndef PV_PK_SPLIT
+#define PV_PK_SPLIT 1  // packed-instruction real split (analysis)
+#endif
+#ifndef PV_PK_PRESTEP
+#define PV_PK_PRESTEP 1  // packed-instruction inverse real-FFT pre-step (synthesis)
+#endif
+
 namespace pv {
 
 // Real-FFT split of bin k (0 <= k <= L) from the natural-order L-point transform in tile.
@@ -49,6 +56,27 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
             tw[c] = lds_ld(&twsl[L]);
         }
     }
+#if PV_PK_SPLIT
+    // packed form, same roundings: S = A + B, D = A - B; H = S/2 = (er, or); G = D/2 =
+    // (-oi, ei); P = (oi tw.y, oi tw.x) = (-G.x tw.y, -G.x tw.x) (sign flips are exact);
+    // T = (fma(or, tw.x, -P.x), fma(or, tw.y, P.y)); X = (er, ei) + T
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        const f2v a = f2v{A[c].x, A[c].y}, b = f2v{Bz[c].x, Bz[c].y}, w = f2v{tw[c].x, tw[c].y};
+        const f2v H = pk_half(pk_add(a, b));
+        const f2v G = pk_half(pk_sub(a, b));
+        f2v P, T;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[1,0]"
+            : "=v"(P) : "v"(G), "v"(w));
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] neg_lo:[0,0,1]"
+            : "=v"(T) : "v"(H), "v"(w), "v"(P));
+        const f2v Xv = pk_add(pk_lo_hi(H, G), T);
+        float Xi = Xv.y;
+        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
+        X[c] = make_float2(Xv.x, Xi);
+    }
+#else
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int i = i0 + c;
@@ -61,6 +89,7 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
         X[c] = make_float2(Xr, Xi);
     }
+#endif
 }
 
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
@@ -199,12 +228,25 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         const int i = lane + 64 * q;
         const float2 A = lds_ld(&baseA[G_::padc(64 * q)]);
         const float2 Bc = lds_ld(&baseB[-G_::padc(64 * q)]);
+        const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
+#if PV_PK_PRESTEP
+        // S = A + B = (fer, di), D = A - B = (dr, fei); V = (dr, di);
+        // R = (di tw.y, -(dr tw.y)); Q = (For, Foi) = V tw.x + R; z = (fer - Foi, fei + For)
+        const f2v a = f2v{A.x, A.y}, b = f2v{Bc.x, Bc.y}, w = f2v{tw.x, tw.y};
+        const f2v S = pk_add(a, b), D = pk_sub(a, b);
+        const f2v V = pk_lo_hi(D, S), W = pk_lo_hi(S, D);
+        f2v R, Q, Z;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1] neg_hi:[1,0]" : "=v"(R) : "v"(V), "v"(w));
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(Q) : "v"(V), "v"(w), "v"(R));
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(Z) : "v"(W), "v"(Q));
+        z[q] = make_float2(Z.x, Z.y);
+#else
         const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
         const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
-        const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
         const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
         const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
         z[q] = make_float2(fer - Foi, fei + For);
+#endif
     }
     wave_lds_sync();
     fft_run<L, true, STORE_LAST>(z, tile, twl, tw0, lane);

@@ -95,6 +95,17 @@ struct RtParams {
     float inv_q;
 };
 
+// harmoniser mix: dst[c][i] = sum_k gain[k] * src[k][c][i]
+struct MixParams {
+    const float* src;
+    long long ldo, ld_voice;
+    int voices;
+    float gain[64];
+    float* dst;
+    long long ld_mix, len;
+    int channels;
+};
+
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
@@ -104,6 +115,7 @@ hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
 size_t synthesis_lds_bytes(int L, int hs);
 hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
                       hipStream_t s);
+hipError_t launch_mix(const MixParams& p, hipStream_t s);
 hipError_t launch_rt(int L, int mode, const RtParams& p, hipStream_t s);
 size_t rt_lds_bytes(int L);
 hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,

@@ -15,6 +15,10 @@
 #include "pv_frame.hpp"
 #include "pv_kernels.h"
 
+#ifndef PV_SYN_GREG
+#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512)
+#endif
+
 namespace pv {
 
 // ------------------------------------------------------------------ K1 STANDARD
@@ -36,7 +40,11 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
     const int BP = p.bins_pad;
 
     const int tid = threadIdx.x, lane = tid & 63;
+    #ifdef PV_NO_RFL_ANA
+    const int w = tid >> 6;
+#else
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
+#endif
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
@@ -303,21 +311,27 @@ __global__ __launch_bounds__(256) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
+#ifndef PV_SYN_WAVES512
+#define PV_SYN_WAVES512 3  // waves per SIMD the L = 512 synthesis is compiled for
+#endif
 template <int L, int MODE, int DT, bool QPOW2 = false>
-__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_synthesis(SynParams p) {
+__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int SPW = N / 64;  // samples per lane per frame
     constexpr int B = L + 1;
-    constexpr bool GREG = ROLA && L <= 512;  // ROLA gains in registers (else LDS float2 reads)
+    constexpr bool GREG = PV_SYN_GREG && ROLA && L <= 512;  // ROLA gains in registers (else LDS)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* twl = reinterpret_cast<float2*>(smem);                     // L
     float2* twsl = twl + L;                                            // L (+2 pad)
     float2* tiles = twsl + (L + 2);                                    // 4 x TILE
-    float* rings = reinterpret_cast<float*>(tiles + 4 * G_::TILE);    // 4 x N
-    float* gainl = rings + 4 * N;                                      // N (unless GREG)
+    float* after_tiles = reinterpret_cast<float*>(tiles + 4 * G_::TILE);
+    // 4 x N tails: ROLA writes them only after the frame loop, into the tile area
+    // (4 TILE float2 >= 4 N floats); the LDS ring of DT = 0 is live throughout
+    float* rings = ROLA ? reinterpret_cast<float*>(tiles) : after_tiles;
+    float* gainl = ROLA ? after_tiles : rings + 4 * N;                 // N (unless GREG)
     float* ekl = gainl + (GREG ? 0 : N);                               // B (+pad)
     unsigned* jkl = reinterpret_cast<unsigned*>(ekl + (B + 3));        // B (+pad)
     int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
@@ -418,25 +432,28 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
     const bool fast = FASTOK && nfr == p.F && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
     if (FASTOK && fast) {
         // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
-        // [vmcnt(D): row u+1 landed, the stores may still be in flight]
-        float2 sv[E + 1];
-        {
-            const float2* srow = specc + (long long)t0 * p.spec_stride;
+        // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
+        // alternate (F is even), so no register copies carry a row across trips.
+        auto step = [&](int u, const f2v (&row)[E + 1]) {
+            float2 sv[E + 1];
 #pragma unroll
-            for (int i = 0; i < E; ++i) sv[i] = srow[lane + 64 * i];
-            sv[E] = srow[L];
-        }
-        for (int u = 0; u < p.F; ++u) {
-            f2v nx[E + 1];
-            const float2* nrow = specc + (long long)(t0 + min(u + 1, p.F - 1)) * p.spec_stride;
-            gload_row<E>(nx, nrow + lane, nrow + L);
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
             float2 z[E];
             synth(u, t0 + u, sv, z);
             ola_regs(z);
             flush_regs(u, std::true_type{});  // exactly D stores
-            vm_wait<D>(nx);
-#pragma unroll
-            for (int i = 0; i <= E; ++i) sv[i] = make_float2(nx[i].x, nx[i].y);
+        };
+        auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
+        f2v ra[E + 1], rb[E + 1];
+        gload_row<E>(ra, rowp(0) + lane, rowp(0) + L);
+        vm_wait<0>(ra);
+        for (int u = 0; u < p.F; u += 2) {
+            gload_row<E>(rb, rowp(u + 1) + lane, rowp(u + 1) + L);
+            step(u, ra);
+            vm_wait<D>(rb);
+            gload_row<E>(ra, rowp(u + 2) + lane, rowp(u + 2) + L);
+            step(u + 1, rb);
+            vm_wait<D>(ra);
         }
     } else {
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
@@ -492,7 +509,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? 3 : 1) void k_sy
         }
     }
     if constexpr (ROLA) {
-        // the run's tail (positions F*hs + j, j < N - hs) -> ring[j]
+        // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
+        __syncthreads();
         float2* r2 = reinterpret_cast<float2*>(ring);
 #pragma unroll
         for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
@@ -538,6 +556,24 @@ __global__ __launch_bounds__(256) void k_seam(SeamParams p) {
     }
 }
 
+// ------------------------------------------------------------------ harmoniser mix
+// Streams the K voice outputs once: each thread sums one sample position over the voices.
+__global__ __launch_bounds__(256) void k_mix(MixParams p) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= p.len) return;
+    const float* src = p.src + (long long)c * p.ldo + i;
+    float acc = 0.0f;
+    for (int k = 0; k < p.voices; ++k) acc = __builtin_fmaf(p.gain[k], src[(long long)k * p.ld_voice], acc);
+    p.dst[(long long)c * p.ld_mix + i] = acc;
+}
+
+hipError_t launch_mix(const MixParams& p, hipStream_t s) {
+    dim3 grid((unsigned)((p.len + 255) / 256), p.channels);
+    hipLaunchKernelGGL(k_mix, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ OVERLAPTEST
 // kernel.cu:289-298: cudaWindow, cufftShift (out-of-place), cufftShift (in place),
 // cudaWindow, cudaOverlapAdd -> out[k] = w[k]^2 x[k] + back[k + hop]
@@ -572,8 +608,10 @@ static size_t ana_lds_compat() {
 // overlap-add at L <= 512 the gains live in registers and gainl is not allocated
 template <int L>
 static size_t syn_lds(int dt) {
+    const int ring_floats = (dt > 0) ? 0 : 4 * 2 * L;               // ROLA: tails alias the tiles
+    const int gain_floats = (PV_SYN_GREG && dt > 0 && L <= 512) ? 0 : 2 * L;  // GREG: gains in registers
     return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) +
-           sizeof(float) * ((dt > 0 && L <= 512) ? 4 : 5) * (2 * L) + sizeof(float) * 4 * (L + 1 + 3);
+           sizeof(float) * (ring_floats + gain_floats) + sizeof(float) * 4 * (L + 1 + 3);
 }
 
 // register overlap-add slots per frame (out hop = 128 DT), 0 = LDS ring

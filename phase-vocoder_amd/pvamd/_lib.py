@@ -8,7 +8,7 @@ import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.abspath(os.path.join(_PKG, "..", ".."))
-LIB_PATH = os.path.join(_PKG, "..", "build", "libpv.so")
+LIB_PATH = os.environ.get("PV_LIB_PATH") or os.path.join(_PKG, "..", "build", "libpv.so")
 HEADER = os.path.join(ROOT, "include", "pv.h")
 
 PV_OK, PV_ERR_ARG, PV_ERR_UNSUPPORTED, PV_ERR_HIP, PV_ERR_NOMEM = range(5)
@@ -103,6 +103,14 @@ def lib():
     L.pv_rt_callback.restype = i
     L.pv_fft_c2c.argtypes = [vp, vp, i, i, i, vp]
     L.pv_fft_c2c.restype = i
+    L.pv_harmonizer_create.argtypes = [ctypes.POINTER(pv_config), ctypes.POINTER(ctypes.c_float), i,
+                                       ctypes.POINTER(vp)]
+    L.pv_harmonizer_create.restype = i
+    L.pv_harmonizer_destroy.argtypes = [vp]
+    L.pv_harmonizer_destroy.restype = None
+    L.pv_harmonize.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, ll, ctypes.POINTER(ctypes.c_float),
+                               vp, ll, vp]
+    L.pv_harmonize.restype = i
     _lib = L
     return L
 

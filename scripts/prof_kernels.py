@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--scale", type=float, default=0.5)
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--mode", default="standard")
+    ap.add_argument("--calib", action="store_true")
     args = ap.parse_args()
     import torch
     from bench import synth_channels_np
@@ -33,6 +34,16 @@ def main():
     for _ in range(args.reps):
         pv.process(x, spec=spec, out=out)
     torch.cuda.synchronize()
+    if args.calib:
+        # traffic calibration: the batched FFT reads and writes exactly 8*n*batch bytes with
+        # the same 8-byte-per-lane global loads / stores as the phase-vocoder kernels
+        from pvamd.fft import fft
+        a = torch.zeros((131072, 512), dtype=torch.complex64, device="cuda:0")
+        b = torch.empty_like(a)
+        for _ in range(args.reps):
+            fft(a, out=b)
+        torch.cuda.synchronize()
+        print("calib bytes", a.numel() * 8)
     print("done", frames)
 
 
