@@ -63,12 +63,23 @@ def synth_channels_np(C, n, seed0):
     return out
 
 
-def cpu_baseline(N, hop_div, effect, scale, n, target_s=10.0):
-    """The CPU oracle (oracle/pvref.c, OpenMP over channels) on a bounded sample."""
+def cpu_baseline(N, hop_div, effect, scale, n, target_s=10.0, single=False):
+    """The CPU oracle (oracle/pvref.c, OpenMP over channels) on a bounded sample; a single
+    stream (single=True) has no channel parallelism and runs on one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pvref  # test infrastructure: used here only as the timed CPU baseline
 
     threads = int(os.environ.get("PV_CPU_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    if single:
+        threads = 1
+        x = synth_channels_np(1, n, 20240)
+        frames = pvref.num_frames(n, N // hop_div)
+        t0 = time.perf_counter()
+        _, used = pvref.std_process_batch(x, N, hop_div, effect, scale, frames, 1)
+        dt = time.perf_counter() - t0
+        return {"value": frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
+                "sample": f"the whole stream ({n} samples, {frames} frames), oracle/pvref.c, "
+                          f"{dt:.1f} s wall"}
     frames = pvref.num_frames(n, N // hop_div)
     probe = synth_channels_np(threads, n, 20240)
     t0 = time.perf_counter()
@@ -95,8 +106,10 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    ap.add_argument("--workload", choices=["batch", "rt"], default="batch",
-                    help="batch: configs[2] (default, the headline line); rt: configs[4]")
+    ap.add_argument("--workload", choices=["c3", "c2", "c4", "rt", "batch"], default="c3",
+                    help="c3 (= batch): configs[2], the headline line (default); c2: configs[1] "
+                         "single 60 s stream, pitch 2.0; c4: configs[3] per-GPU slice (1024 ch, "
+                         "N=2048 hop=512, pitch 1.5); rt: configs[4] real-time mode")
     args = ap.parse_args()
     if args.workload == "rt":
         return bench_rt(args)
@@ -112,12 +125,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
 
-    from pvamd import PhaseVocoder, STANDARD, TIME_SHIFT
+    from pvamd import PITCH_SHIFT, PhaseVocoder, STANDARD, TIME_SHIFT
 
-    N, hop_div, scale = 1024, 4, 0.5
-    n = int(round(args.seconds * SR))
-    C = args.channels
-    pv = PhaseVocoder(N, TIME_SHIFT, scale, hop_div, mode=STANDARD, max_channels=C,
+    wl = "c3" if args.workload == "batch" else args.workload
+    # (N, hop_div, effect, scale, seconds, channels per GPU, description)
+    WL = {"c3": (1024, 4, TIME_SHIFT, 0.5, args.seconds, args.channels,
+                 "BASELINE configs[2]: 1024 mono ch x 10 s per GPU, N=1024 hop=256, "
+                 "PV_STANDARD time-stretch 0.5"),
+          "c2": (1024, 4, PITCH_SHIFT, 2.0, 60.0, 1,
+                 "BASELINE configs[1]: single mono 44.1 kHz stream x 60 s, N=1024 hop=256, "
+                 "PV_STANDARD pitch 2.0"),
+          "c4": (2048, 4, PITCH_SHIFT, 1.5, args.seconds, args.channels,
+                 "BASELINE configs[3] per-GPU slice: 1024 mono ch x 10 s per GPU, N=2048 hop=512, "
+                 "PV_STANDARD pitch 1.5 (8192 ch on 8 GPUs)")}
+    N, hop_div, effect, scale, seconds, C, wl_desc = WL[wl]
+    n = int(round(seconds * SR))
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C,
                       max_frames=pv_frames(n, N // hop_div), device=local)
     frames = pv.num_frames(n)
     tables = None
@@ -181,7 +204,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(N, hop_div, ord("t"), scale, n)
+            cpu = cpu_baseline(N, hop_div, ord(effect), scale, n, single=(C == 1))
         except Exception as e:  # reported, never fatal for the GPU number
             cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                    "sample": f"failed: {e}"}
@@ -192,8 +215,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (3 sines U[55,4000] Hz a=0.1 + U(+-1e-3) noise, seed 20240+ch)",
-            "config": {"workload": "BASELINE configs[2]: 1024 mono ch x 10 s per GPU, N=1024 hop=256, "
-                                   "PV_STANDARD time-stretch 0.5",
+            "config": {"workload": wl_desc,
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
                        "out_hop": hop_s, "parallelism": f"channel-shard x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -187,6 +187,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.tw = h->d_tw_ana;
     p.tws = h->d_tws_ana;
     p.ek = h->d_ek;
+    p.ek_lane = (64 % h->cfg.hop_div == 0 && h->bins >= 64) ? 1 : 0;
     p.spec = reinterpret_cast<float2*>(spec);
     p.ld_spec = ld_spec;
     p.spec_stride = h->spec_stride;
@@ -204,7 +205,8 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
 // geometry (the harmoniser's voices share one scan); nullptr = scan here.
 pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int C, int frames,
                          const float* ola_in, long long ld_ola, float* out, long long ldo,
-                         bool have_runsum, hipStream_t s, const int* carry_from = nullptr) {
+                         bool have_runsum, hipStream_t s, const int* carry_from = nullptr,
+                         bool force_scan = false) {
     if (C == 0 || frames == 0) {
         return PV_OK;
     }
@@ -215,7 +217,10 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
         return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
     const int nruns = nruns_of(h, frames);
     const float2* sp = reinterpret_cast<const float2*>(spec);
-    if (h->mode == PV_MODE_STANDARD && carry_from == nullptr) {
+    // q = 1 (e.g. pitch 2.0): the output phase rho (phi + 2 pi M) is independent of the
+    // unwrap count M mod 1, so no scan is needed
+    const bool need_scan = h->mode == PV_MODE_STANDARD && (h->q > 1 || force_scan);
+    if (need_scan && carry_from == nullptr) {
         pv::ScanParams sc{};
         sc.spec = sp;
         sc.ld_spec = ld_spec;
@@ -239,7 +244,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.F = h->F;
     p.nruns = nruns;
     p.bins_pad = h->bins_pad;
-    p.carry = carry_from ? carry_from : h->d_carry;
+    p.carry = carry_from ? carry_from : (need_scan ? h->d_carry : nullptr);
     p.ek = h->d_ek;
     p.jk_mod = h->d_jk_mod;
     p.src_first = h->d_src_first;
@@ -538,7 +543,7 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     if (st != PV_OK) return st;
     DeviceGuard g(h->cfg.device);
     hipStream_t s = (hipStream_t)stream;
-    const bool std_mode = (h->mode == PV_MODE_STANDARD);
+    const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
     if (st != PV_OK) return st;
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
@@ -995,7 +1000,8 @@ pv_status pv_harmonize(pv_harmonizer* hz, const float* x, long long ldx, long lo
     hipStream_t s = (hipStream_t)stream;
     st = do_analysis(h0, x, ldx, n_samples, channels, frames, spec, ld_spec, true, s);
     if (st != PV_OK) return st;
-    st = do_resynthesis(h0, spec, ld_spec, channels, frames, nullptr, 0, voices_out, ldo, true, s);
+    st = do_resynthesis(h0, spec, ld_spec, channels, frames, nullptr, 0, voices_out, ldo, true, s,
+                        nullptr, /*force_scan: other voices read h0's carries*/ true);
     if (st != PV_OK) return st;
     for (int k = 1; k < K; ++k) {
         st = do_resynthesis(hz->voices[k], spec, ld_spec, channels, frames, nullptr, 0,

@@ -6,7 +6,7 @@
 #include "pv_device.hpp"
 
 #ifndef PV_PK_SPLIT
-#define PV_PK_SPLIT 1  // packed-instruction real split (analysis)
+#define PV_PK_SPLIT 0  // packed-instruction real split (analysis): measured slower (latency)
 #endif
 #ifndef PV_PK_PRESTEP
 #define PV_PK_PRESTEP 1  // packed-instruction inverse real-FFT pre-step (synthesis)

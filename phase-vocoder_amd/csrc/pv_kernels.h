@@ -14,6 +14,7 @@ struct AnaParams {
     const float2* tw;       // stage-major twiddles of the L-point FFT (L entries)
     const float2* tws;      // real-split twiddles e^{-2 pi i k / (2L)}, k <= L
     const float* ek;        // expected advance (STANDARD), bins
+    int ek_lane;            // 64 % hop_div == 0: e_k = ek[k mod 64] (per-lane constant)
     float2* spec;
     long long ld_spec;
     int spec_stride;

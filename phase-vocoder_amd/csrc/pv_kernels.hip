@@ -15,6 +15,9 @@
 #include "pv_frame.hpp"
 #include "pv_kernels.h"
 
+#ifndef PV_ANA_CH
+#define PV_ANA_CH 3  // analysis: bins per batch of LDS reads + atan2 chains
+#endif
 #ifndef PV_SYN_GREG
 #define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512)
 #endif
@@ -25,8 +28,13 @@ namespace pv {
 // One wave = one run of F consecutive frames (plus the halo frame t0-1, transformed only
 // for its phase).  The unwrap decision m(t) = f(phi[t], phi[t-1]) is accumulated in
 // registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
-template <int L>
-__global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_std_analysis(AnaParams p) {
+// EKL: the expected advance e_k from an LDS table; otherwise (64 a multiple of the hop
+// divisor, so e_k depends on k mod 64 only) one register per lane, e_k = ek[lane].
+#ifndef PV_ANA_WAVES512
+#define PV_ANA_WAVES512 4
+#endif
+template <int L, bool EKL>
+__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? 2 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -48,7 +56,11 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
-    for (int i = tid; i < B; i += 256) { twsl[i] = p.tws[i]; ekl[i] = p.ek[i]; }
+    for (int i = tid; i < B; i += 256) {
+        twsl[i] = p.tws[i];
+        if (EKL) ekl[i] = p.ek[i];
+    }
+    const float e_lane = EKL ? 0.0f : p.ek[tid & 63];
     for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
     __syncthreads();
     const int run = blockIdx.x * 4 + w, c = blockIdx.y;
@@ -83,7 +95,7 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
         (void)srow;
         fft_run<L, false>(z, tile, twl, tw0, lane);
         // bins in chunks of CH (bounded live registers), all reads of a chunk batched
-        constexpr int CH = 3;
+        constexpr int CH = PV_ANA_CH;
 #pragma unroll
         for (int i0 = 0; i0 <= E; i0 += CH) {
             float2 X[CH];
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(256, (L <= 512) ? 4 : (L == 1024) ? 2 : 1) void k_s
                     const float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                     // bin L (i = E) has the same value and address on every lane
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
-                    const int m = unwrap_count(ph, phprev[i], lds_ld(&ekl[k]));
+                    const int m = unwrap_count(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
                     if (u == 0 && rec != nullptr && (i < E || lane == 0)) rec[BP + k] = m;
                     sacc[i] += (u == 0) ? 0 : m;
                 }
@@ -261,31 +273,57 @@ __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
     dst[p.bins_pad + k] = m0;
 }
 
-// carry[run] = M(t0) = sum over earlier runs of (m0 + S) + m0(run)
-__global__ __launch_bounds__(256) void k_carry(ScanParams p) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
+// carry[run] = M(t0) = sum over earlier runs of (m0 + S) + m0(run).
+// Block = 64 bins x SEG run segments (one wave each): pass 1 sums each segment, the
+// segment offsets are scanned in LDS, pass 2 rescans the segment writing carries.  All
+// integer, so the split of the scan changes no bit.
+template <int SEG>
+__global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
+    __shared__ int tot[SEG][64];
+    const int lane = threadIdx.x & 63;
+    const int sg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = blockIdx.x * 64 + lane;
     const int c = blockIdx.y;
-    if (k > p.L) return;
     const int BP = p.bins_pad;
-    const int* rs = p.runsum + (long long)c * p.nruns * 2 * BP + k;
-    int* cr = p.carry + (long long)c * p.nruns * BP + k;
-    int M = 0;
-    int run = 0;
-    for (; run + 4 <= p.nruns; run += 4) {
-        int s[4], m[4];
+    const int per = (p.nruns + SEG - 1) / SEG;
+    const int r0 = min(p.nruns, sg * per), r1 = min(p.nruns, r0 + per);
+    const bool on = k <= p.L;
+    const int* rs = p.runsum + (long long)c * p.nruns * 2 * BP + (on ? k : 0);
+    int* cr = p.carry + (long long)c * p.nruns * BP + (on ? k : 0);
+    int T = 0;
+    int run = r0;
+    for (; run + 4 <= r1; run += 4) {
+        int a[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            s[j] = rs[(long long)(run + j) * 2 * BP];
-            m[j] = rs[(long long)(run + j) * 2 * BP + BP];
+            a[2 * j] = rs[(long long)(run + j) * 2 * BP];
+            a[2 * j + 1] = rs[(long long)(run + j) * 2 * BP + BP];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T += a[j];
+    }
+    for (; run < r1; ++run) T += rs[(long long)run * 2 * BP] + rs[(long long)run * 2 * BP + BP];
+    tot[sg][lane] = T;
+    __syncthreads();
+    int M = 0;
+    for (int j = 0; j < sg; ++j) M += tot[j][lane];
+    if (!on) return;
+    run = r0;
+    for (; run + 4 <= r1; run += 4) {
+        int sv[4], mv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sv[j] = rs[(long long)(run + j) * 2 * BP];
+            mv[j] = rs[(long long)(run + j) * 2 * BP + BP];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            M += m[j];
+            M += mv[j];
             cr[(long long)(run + j) * BP] = M;
-            M += s[j];
+            M += sv[j];
         }
     }
-    for (; run < p.nruns; ++run) {
+    for (; run < r1; ++run) {
         M += rs[(long long)run * 2 * BP + BP];
         cr[(long long)run * BP] = M;
         M += rs[(long long)run * 2 * BP];
@@ -371,8 +409,9 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     int M[E + 1];
     float phprev[E + 1];
     if (MODE != 1 && nfr > 0) {
-        const int* cr = p.carry + ((long long)c * p.nruns + run) * p.bins_pad;
-        PV_FOR_BINS(E, lane, { M[i] = cr[k]; phprev[i] = 0.0f; })
+        // no carries when the output phase does not depend on the unwrap count (q = 1)
+        const int* cr = p.carry ? p.carry + ((long long)c * p.nruns + run) * p.bins_pad : nullptr;
+        PV_FOR_BINS(E, lane, { M[i] = cr ? cr[k] : 0; phprev[i] = 0.0f; })
     }
 
     // ROLA state: acc[c] = run positions u*hs + 128 c + 2 lane + {0,1}; gains likewise
@@ -597,8 +636,8 @@ hipError_t launch_overlap_test(const float* in, const float* win, const float* b
 
 // ------------------------------------------------------------------ launchers
 template <int L>
-static size_t ana_lds_std(int) {
-    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + L + 1);
+static size_t ana_lds_std(bool ekl) {
+    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
 }
 template <int L>
 static size_t ana_lds_compat() {
@@ -646,7 +685,8 @@ size_t synthesis_lds_bytes(int L, int hs) {
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
     PV_DISPATCH_L(L, {
-        hipLaunchKernelGGL(k_std_analysis<LL>, grid, dim3(256), ana_lds_std<LL>(p.bins_pad), s, p);
+        if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+        else hipLaunchKernelGGL((k_std_analysis<LL, true>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });
     return hipGetLastError();
 }
@@ -666,8 +706,13 @@ hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s) {
 }
 
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
-    dim3 grid((p.L + 1 + 255) / 256, channels);
-    hipLaunchKernelGGL(k_carry, grid, dim3(256), 0, s, p);
+    // segments per (channel, 64-bin block): enough waves to fill the chip when the batch
+    // has few channels, few passes over the records when it has many
+    dim3 grid((p.L + 1 + 63) / 64, channels);
+    const long long blocks = (long long)grid.x * channels;
+    if (blocks >= 2048 || p.nruns < 64) hipLaunchKernelGGL(k_carry<1>, grid, dim3(64), 0, s, p);
+    else if (blocks >= 256) hipLaunchKernelGGL(k_carry<4>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_carry<16>, grid, dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
