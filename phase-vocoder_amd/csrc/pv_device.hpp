@@ -116,6 +116,18 @@ __device__ __forceinline__ void gload_pairs(f2v (&xr)[E], const float* src) {
                      : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
+// the last D pairs of gload_pairs<E>: registers q = E-D .. E-1
+template <int D, int E>
+__device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        constexpr int Q0 = E - D;
+        const int q = Q0 + j;
+        const float* pq = src + 1024 * (q >> 3);
+        asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
+                     : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+    }
+}
 // one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and bin L (the
 // same address on every lane) from rowL
 template <int E>

@@ -15,6 +15,12 @@
 #include "pv_frame.hpp"
 #include "pv_kernels.h"
 
+#ifndef PV_NT_SPEC
+#define PV_NT_SPEC 1  // non-temporal spectrum row stores in the analysis
+#endif
+#ifndef PV_ANA_SHIFT
+#define PV_ANA_SHIFT 1  // shifted-register input when hop = 128 D (k_std_analysis<L, false, D>)
+#endif
 #ifndef PV_ANA_CH
 #define PV_ANA_CH 3  // analysis: bins per batch of LDS reads + atan2 chains
 #endif
@@ -33,7 +39,10 @@ namespace pv {
 #ifndef PV_ANA_WAVES512
 #define PV_ANA_WAVES512 4
 #endif
-template <int L, bool EKL>
+// D > 0: hop = 128 D samples, so frame u+1's register q is frame u's register q + D and a
+// frame costs only its D new sample pairs per lane (the other E - D are shifted in
+// registers): 1/E of the frame's bytes leave L2 instead of all of them.
+template <int L, bool EKL, int D = 0>
 __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? 2 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
@@ -111,7 +120,13 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
                     // the phase, which drives the unwrap decisions, stays bit-exact
                     const float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                     // bin L (i = E) has the same value and address on every lane
+#if PV_NT_SPEC
+                    // non-temporal: the rows are read back by another launch, long after
+                    // they would have left L2 (measured: analysis -7 %)
+                    __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+#else
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
+#endif
                     const int m = unwrap_count(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
                     if (u == 0 && rec != nullptr && (i < E || lane == 0)) rec[BP + k] = m;
                     sacc[i] += (u == 0) ? 0 : m;
@@ -149,7 +164,25 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     // [vmcnt(E + 1): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
     // The prefetch index is clamped (the last trip reloads its own frame), so the loads
     // and stores are unconditional and the count is exact (gload_pairs / vm_wait).
-    if (L <= 1024 && ufast > 0) {
+    if constexpr (D > 0) {
+        static_assert(D < E, "shifted input: hop < N / 2");
+        if (ufast > 0) {
+            float2 xr[E], z[E];
+            load_fast(0, xr);
+            window(xr, z);
+            for (int u = 0; u < ufast; ++u) {
+                f2v xv[D];  // the D new pairs of frame u+1: registers E-D .. E-1
+                gload_tail<D, E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
+                frame(u, z, std::false_type{});  // exactly E + 1 row stores (+ records at u = 0)
+                vm_wait<E + 1>(xv);
+#pragma unroll
+                for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) xr[E - D + j] = make_float2(xv[j].x, xv[j].y);
+                window(xr, z);
+            }
+        }
+    } else if (L <= 1024 && ufast > 0) {
         float2 z[E];
         {
             float2 xr[E];
@@ -685,7 +718,13 @@ size_t synthesis_lds_bytes(int L, int hs) {
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
     PV_DISPATCH_L(L, {
-        if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+        const int d = (p.aligned && p.hop % 128 == 0) ? p.hop / 128 : 0;
+        if (PV_ANA_SHIFT && p.ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
+            constexpr int E_ = LL / 64;  // D < E (instantiated for every L, run for the checked ones)
+            if (d == 1) hipLaunchKernelGGL((k_std_analysis<LL, false, (1 < E_) ? 1 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+            else if (d == 2) hipLaunchKernelGGL((k_std_analysis<LL, false, (2 < E_) ? 2 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+            else hipLaunchKernelGGL((k_std_analysis<LL, false, (4 < E_) ? 4 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+        } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
         else hipLaunchKernelGGL((k_std_analysis<LL, true>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });
     return hipGetLastError();
