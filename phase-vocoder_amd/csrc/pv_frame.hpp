@@ -128,12 +128,16 @@ struct SynLds {
 // FFT's last-pass registers z (point lane + 64 last_slot(idx)).
 // QPOW2: the output-phase denominator q is a power of two <= 2^24 (compile-time path);
 // otherwise the generic path handles any q the handle accepts.
-template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false>
+// KREG: the per-bin unwrap constants e_k, (p j_k) mod q come from the caller's registers
+// (ekr, jkr: frame-invariant, loaded once per wave) instead of LDS reads every frame.
+template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
                                             const SynLds& tb, const float2 (&tw0)[Geo<L>::E],
-                                            float2* tile, int lane, float2 (&z)[Geo<L>::E]) {
+                                            float2* tile, int lane, float2 (&z)[Geo<L>::E],
+                                            const float (&ekr)[Geo<L>::E + 1],
+                                            const unsigned (&jkr)[Geo<L>::E + 1]) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int B = L + 1;
@@ -145,11 +149,16 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     (void)ekl; (void)jkl; (void)srcl; (void)B;
     float mag[E + 1], ph[E + 1];
     PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
+    float2 Yr[E + 1];  // Y of the lane's bins k = lane + 64 i (+ bin L on lane 0)
     if constexpr (MODE != 1) {
         float phc[E + 1];
         float ekv[E + 1];
         unsigned jkv[E + 1];
-        PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
+        if constexpr (KREG) {
+            PV_FOR_BINS(E, lane, { ekv[i] = ekr[i]; jkv[i] = jkr[i]; })
+        } else {
+            PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
+        }
         PV_FOR_BINS(E, lane, {
             const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
             M[i] += add_decision ? mm : 0;
@@ -198,7 +207,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             PV_FOR_BINS(E, lane, {
                 float2 y = Y[i];
                 if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
-                tile[G_::pad(k)] = y;
+                Yr[i] = y;
             })
         } else {
             PV_FOR_BINS(E, lane, {
@@ -206,7 +215,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                 sincos_rev(phc[i], &sn, &cs);
                 float2 y = make_float2(mag[i] * cs, mag[i] * sn);
                 if (k == 0 || k == L) y.y = 0.0f;
-                tile[G_::pad(k)] = y;
+                Yr[i] = y;
             })
         }
     } else {
@@ -216,19 +225,28 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             const float xr = mag[i] * cs;                 // kernel.cu:127
             float2 y = make_float2(xr, xr * sn);          // kernel.cu:128 (updated x)
             if (k == 0 || k == L) y.y = 0.0f;
-            tile[G_::pad(k)] = y;
+            Yr[i] = y;
         })
     }
-    wave_lds_sync();
-    // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q
-    const float2* baseA = tile + G_::pad(lane);
-    const float2* baseB = tile + G_::pad(L - lane);
+    // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q, from
+    // A = Y[i] (this lane's register q) and B = Y[L - i].  For lane l >= 1, bin L - i =
+    // (64 - l) + 64 (E - 1 - q) is register E-1-q of lane 64 - l: a lane reversal by
+    // ds_bpermute (crossbar only, no LDS memory traffic); lane 0's partners are its own
+    // registers E - q (bin L - 64 q, q = 0 -> bin L).
+    const int src_lane = ((64 - lane) & 63) << 2;
+    float2 Bp[E];
 #pragma unroll
     for (int q = 0; q < E; ++q) {
-        const int i = lane + 64 * q;
-        const float2 A = lds_ld(&baseA[G_::padc(64 * q)]);
-        const float2 Bc = lds_ld(&baseB[-G_::padc(64 * q)]);
-        const float2 tw = lds_ld(&twsl[i]);              // e^{-2 pi i k/N}
+        const float2 o = Yr[E - 1 - q];
+        Bp[q].x = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.x)));
+        Bp[q].y = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.y)));
+    }
+    wave_lds_sync();  // the FFT's first tile store stays after the reads above (MODE 2)
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        const float2 A = Yr[q];
+        const float2 Bc = (lane == 0) ? Yr[E - q] : Bp[q];
+        const float2 tw = lds_ld(&twsl[lane + 64 * q]);   // e^{-2 pi i k/N}, k = lane + 64 q
 #if PV_PK_PRESTEP
         // S = A + B = (fer, di), D = A - B = (dr, fei); V = (dr, di);
         // R = (di tw.y, -(dr tw.y)); Q = (For, Foi) = V tw.x + R; z = (fer - Foi, fei + For)

@@ -382,6 +382,9 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
+#ifndef PV_SYN_KREG
+#define PV_SYN_KREG 0  // measured: no gain over the LDS reads
+#endif
 #ifndef PV_SYN_WAVES512
 #define PV_SYN_WAVES512 3  // waves per SIMD the L = 512 synthesis is compiled for
 #endif
@@ -460,12 +463,18 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
         }
     }
 
+    // unwrap constants of the lane's bins in registers for the whole run (ROLA kernels
+    // have VGPRs to spare below their LDS-bound occupancy)
+    constexpr bool KREG = ROLA && MODE == 0 && PV_SYN_KREG;  // pitch (MODE 2) would spill
+    float ekr[E + 1];
+    unsigned jkr[E + 1];
+    if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&ekl[k]); jkr[i] = lds_ld(&jkl[k]); })
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)

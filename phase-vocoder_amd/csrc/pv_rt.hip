@@ -141,7 +141,9 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
         // ---- processing + resynthesis: time samples to tile (natural order)
         const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
         const unsigned tq = QPOW2 ? ((t + 1u) & (q32 - 1u)) : ((t + 1u) % q32);
-        synth_frame<L, MODE, true, QPOW2>(sv, true, tq, M, phprev, pmap, stb, tw0, tile, lane, z);
+        float ekr[E + 1];       // unused (KREG = false)
+        unsigned jkr[E + 1];
+        synth_frame<L, MODE, true, QPOW2>(sv, true, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
         // ---- overlap-add, emit the out hop, shift
         const float* ty = reinterpret_cast<const float*>(tile);
         float nv[SPW];
