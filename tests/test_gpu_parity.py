@@ -206,3 +206,24 @@ def test_odd_output_stride(cuda, mode):
     dense, _ = pv.process(to_dev(xs))
     assert torch.equal(out, dense)
     assert torch.all(big[:, olen:] == 7.0)  # nothing written past the row
+
+
+@pytest.mark.parametrize("F", [8, 16, 32, 48, 64])
+@pytest.mark.parametrize("effect,scale", [(TIME_SHIFT, 0.5), (PITCH_SHIFT, 1.5)])
+def test_run_length_geometries(cuda, monkeypatch, F, effect, scale):
+    """Every frames-per-run the handle may pick (F = 48 for config-3-sized batches) gives
+    the oracle's output; run boundaries only move the seams (<= 1e-6 between runs)."""
+    N, hop_div, C = 1024, 4, 3
+    xs = np.stack([synth(110250, 20240 + c) for c in range(C)])
+    monkeypatch.setenv("PV_RUN_FRAMES", str(F))
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=440)
+    assert pv.frames_per_run == F
+    out, _ = pv.process(to_dev(xs))
+    g = out.cpu().numpy()
+    ref, _ = pvref.std_process_batch(xs, N, hop_div, ord(effect), scale)
+    for c in range(C):
+        assert rms(g[c], ref[c]) <= RMS_TOL, f"F={F} ch{c}"
+    monkeypatch.setenv("PV_RUN_FRAMES", "16")
+    pv16 = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=440)
+    out16, _ = pv16.process(to_dev(xs))
+    assert np.abs(out16.cpu().numpy() - g).max() <= 1e-6
