@@ -207,13 +207,22 @@ __device__ __forceinline__ void sincos_pv(float x, float* sn, float* cs) {
     *cs = ((q + 1) & 2) ? -cv : cv;
 }
 
+#ifndef PV_HW_REDUCE
+#define PV_HW_REDUCE 1  // measured: synthesis -2.5 %
+#endif
 // sin/cos of 2 pi rev.  Default: the hardware v_sin_f32 / v_cos_f32 (inputs in
 // revolutions, quarter-rate transcendental) after an exact reduction to [-1/2, 1/2]
 // (rev - rint(rev) is exact for |rev| < 2^23); PV_SOFT_SINCOS selects the polynomial
 // sincos_pv.  Synthesis parity is tolerance based, so either is in
 // contract; the GPU tests bound the end-to-end error.
 __device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
+#if PV_HW_REDUCE
+    // v_sin/v_cos reduce their input themselves over [-256, 256] revolutions; every
+    // caller passes |rev| < 4 (output phases are carried reduced)
+    const float r = rev;
+#else
     const float r = rev - __builtin_rintf(rev);
+#endif
 #ifdef PV_SOFT_SINCOS
     sincos_pv(r * kTwoPi, sn, cs);
 #else

@@ -109,6 +109,7 @@ struct PhaseMap {
     unsigned q, p_mod;
     int q_pow2;
     float inv_q;
+    float p_over_q;  // (p mod q) / q (RACC)
 };
 
 // LDS tables of the synthesis side (see the kernels' carve-up)
@@ -130,7 +131,12 @@ struct SynLds {
 // otherwise the generic path handles any q the handle accepts.
 // KREG: the per-bin unwrap constants e_k, (p j_k) mod q come from the caller's registers
 // (ekr, jkr: frame-invariant, loaded once per wave) instead of LDS reads every frame.
-template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false>
+// RACC (QPOW2 with q <= 4096): M[i] carries the float bits of R = ((p M) mod q) / q, the
+// unwrap count's output-phase offset in revolutions, updated as fract(R - m p/q), and jkl
+// holds (p j_k mod q) / q as floats; every value is a multiple of 1/q below 2^12, so all of
+// it is exact in fp32 and equals the integer path's offset up to whole revolutions (which
+// sin/cos ignore), for 3 VALU operations per bin less.
+template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
@@ -159,6 +165,21 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         } else {
             PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
         }
+        if constexpr (RACC) {
+            const float npq = -pm.p_over_q;  // -(p mod q) / q
+            const float tqf = (float)tq;
+            PV_FOR_BINS(E, lane, {
+                // m = -rint(dev); R <- fract(R - m p/q) = fract(R + rint(dev) p/q)
+                const float d = (ph[i] - phprev[i]) - ekv[i];
+                const float mr = __builtin_rintf(d * kInv2Pi);
+                float R = __int_as_float(M[i]);
+                if (add_decision) R = __builtin_amdgcn_fractf(__builtin_fmaf(mr, npq, R));
+                M[i] = __float_as_int(R);
+                phprev[i] = ph[i];
+                const float tj = __builtin_amdgcn_fractf(tqf * __uint_as_float(jkv[i]));
+                phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], R + tj);
+            })
+        } else {
         PV_FOR_BINS(E, lane, {
             const int mm = unwrap_count(ph[i], phprev[i], ekv[i]);
             M[i] += add_decision ? mm : 0;
@@ -187,6 +208,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                 phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], (float)(x % qq) * pm.inv_q);
             })
         }
+        }  // !RACC
         if constexpr (MODE == 2) {
             float2 Y[E + 1];
             PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })

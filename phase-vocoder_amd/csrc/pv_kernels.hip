@@ -382,6 +382,9 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
+#ifndef PV_REV_ACC
+#define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
+#endif
 #ifndef PV_SYN_KREG
 #define PV_SYN_KREG 0  // measured: no gain over the LDS reads
 #endif
@@ -411,6 +414,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
     const int hs = p.hs;
     const int TL = N - hs;
+    constexpr bool RACC = QPOW2 && MODE != 1 && PV_REV_ACC;  // host: QPOW2 only for q <= 4096
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
@@ -422,7 +426,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     if (MODE != 1) {
         for (int i = tid; i < B; i += 256) {
             ekl[i] = p.ek[i];
-            jkl[i] = p.jk_mod[i];
+            // RACC: (p j_k mod q) / q as a float (exact: q <= 4096)
+            jkl[i] = RACC ? __float_as_uint((float)p.jk_mod[i] * p.inv_q) : p.jk_mod[i];
             if (MODE == 2) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
         }
     }
@@ -447,7 +452,16 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     if (MODE != 1 && nfr > 0) {
         // no carries when the output phase does not depend on the unwrap count (q = 1)
         const int* cr = p.carry ? p.carry + ((long long)c * p.nruns + run) * p.bins_pad : nullptr;
-        PV_FOR_BINS(E, lane, { M[i] = cr ? cr[k] : 0; phprev[i] = 0.0f; })
+        if constexpr (RACC) {
+            const unsigned qm = (unsigned)p.q - 1u;
+            PV_FOR_BINS(E, lane, {
+                const unsigned mq = cr ? ((unsigned)p.p_mod * ((unsigned)cr[k] & qm)) & qm : 0u;
+                M[i] = __float_as_int((float)mq * p.inv_q);
+                phprev[i] = 0.0f;
+            })
+        } else {
+            PV_FOR_BINS(E, lane, { M[i] = cr ? cr[k] : 0; phprev[i] = 0.0f; })
+        }
     }
 
     // ROLA state: acc[c] = run positions u*hs + 128 c + 2 lane + {0,1}; gains likewise
@@ -469,12 +483,13 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     float ekr[E + 1];
     unsigned jkr[E + 1];
     if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&ekl[k]); jkr[i] = lds_ld(&jkl[k]); })
-    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q};
+    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
+                        (float)p.p_mod * p.inv_q};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
@@ -803,7 +818,7 @@ static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParam
 // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
-    const bool qp = p.q_pow2 && p.q <= (1ull << 24);
+    const bool qp = p.q_pow2 && p.q <= (PV_REV_ACC ? 4096ull : (1ull << 24));
     const int dt = (mode == 1 || qp) ? syn_dt(L, p.hs) : 0;
     if (mode == 0) return qp ? launch_synthesis_mode<0, true>(L, dt, grid, p, s)
                              : launch_synthesis_mode<0, false>(L, dt, grid, p, s);
