@@ -32,7 +32,11 @@ __device__ __forceinline__ float2 real_split(const float2* tile, const float2* _
 }
 
 // Bins i0 .. i0+CH-1 of a lane (reads batched; entries past E are dummies).
-template <int L, int CH>
+// TWICE: X is returned scaled by exactly 2 (the four halvings dropped).  Scaling by a
+// power of two commutes with every rounding here, so 2X is bit-exactly twice the
+// contract's X and atan2 of it is the contract's phase bit for bit (a = min/max and the
+// sign tests are scale-free); the caller halves the magnitude.
+template <int L, int CH, bool TWICE = false>
 __device__ __forceinline__ void split_chunk(const float2* tile, const float2* twsl, int lane, int i0,
                                             float2 (&X)[CH]) {
     using G_ = Geo<L>;
@@ -80,10 +84,11 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int i = i0 + c;
-        const float er = 0.5f * (A[c].x + Bz[c].x);
-        const float ei = 0.5f * (A[c].y - Bz[c].y);
-        const float orr = 0.5f * (A[c].y + Bz[c].y);
-        const float oi = 0.5f * (Bz[c].x - A[c].x);
+        constexpr float h = TWICE ? 1.0f : 0.5f;
+        const float er = h * (A[c].x + Bz[c].x);
+        const float ei = h * (A[c].y - Bz[c].y);
+        const float orr = h * (A[c].y + Bz[c].y);
+        const float oi = h * (Bz[c].x - A[c].x);
         float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
         float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
@@ -270,12 +275,13 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         const float2 Bc = (lane == 0) ? Yr[E - q] : Bp[q];
         const float2 tw = lds_ld(&twsl[lane + 64 * q]);   // e^{-2 pi i k/N}, k = lane + 64 q
 #if PV_PK_PRESTEP
-        // S = A + B = (fer, di), D = A - B = (dr, fei); V = (dr, di);
+        // V = (dr, di) = (A.x - B.x, A.y + B.y), W = (fer, fei) = (A.x + B.x, A.y - B.y):
+        // one v_pk_add each, the sign flips by neg_lo / neg_hi;
         // R = (di tw.y, -(dr tw.y)); Q = (For, Foi) = V tw.x + R; z = (fer - Foi, fei + For)
         const f2v a = f2v{A.x, A.y}, b = f2v{Bc.x, Bc.y}, w = f2v{tw.x, tw.y};
-        const f2v S = pk_add(a, b), D = pk_sub(a, b);
-        const f2v V = pk_lo_hi(D, S), W = pk_lo_hi(S, D);
-        f2v R, Q, Z;
+        f2v V, W, R, Q, Z;
+        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(V) : "v"(a), "v"(b));
+        asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(W) : "v"(a), "v"(b));
         asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1] neg_hi:[1,0]" : "=v"(R) : "v"(V), "v"(w));
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(Q) : "v"(V), "v"(w), "v"(R));
         asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(Z) : "v"(W), "v"(Q));

@@ -18,6 +18,12 @@
 #ifndef PV_NT_SPEC
 #define PV_NT_SPEC 1  // non-temporal spectrum row stores in the analysis
 #endif
+#ifndef PV_SPLIT2X
+#define PV_SPLIT2X 1  // real split without its four halvings (split_chunk TWICE): analysis -2 %
+#endif
+#if PV_SPLIT2X && PV_PK_SPLIT
+#error "PV_SPLIT2X is implemented for the scalar real split only"
+#endif
 #ifndef PV_ANA_SHIFT
 #define PV_ANA_SHIFT 1  // shifted-register input when hop = 128 D (k_std_analysis<L, false, D>)
 #endif
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
 #pragma unroll
         for (int i0 = 0; i0 <= E; i0 += CH) {
             float2 X[CH];
-            split_chunk<L, CH>(tile, twsl, lane, i0, X);
+            split_chunk<L, CH, PV_SPLIT2X>(tile, twsl, lane, i0, X);
 #pragma unroll
             for (int c2 = 0; c2 < CH; ++c2) {
                 const int i = i0 + c2;
@@ -118,7 +124,8 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
                 if constexpr (!HALO) {
                     // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
                     // the phase, which drives the unwrap decisions, stays bit-exact
-                    const float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    if (PV_SPLIT2X) mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
                     // bin L (i = E) has the same value and address on every lane
 #if PV_NT_SPEC
                     // non-temporal: the rows are read back by another launch, long after
