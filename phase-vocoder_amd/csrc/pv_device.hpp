@@ -150,6 +150,9 @@ __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
     return t;
 }
 
+#ifndef PV_ATAN_IEEE_DIV
+#define PV_ATAN_IEEE_DIV 0  // must match the oracle's contract (it uses the division-free form)
+#endif
 // atan2 of the contract (oracle pvr_atan2f); atan(a) = a*P(a^2), |err| <= 2.7e-7 rad.
 __device__ __forceinline__ float atan2_pv(float y, float x) {
     float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
@@ -164,7 +167,20 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(mx) : "v"(x), "v"(y));
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
 #endif
+#if PV_ATAN_IEEE_DIV
     float a = mn / mx;  // IEEE division (-fhip-fp32-correctly-rounded-divide-sqrt)
+#else
+    // a = mn / mx by the contract's division-free reciprocal (oracle pvr_atan2f): integer
+    // seed + three fmaf Newton steps + one product (8 VALU, no v_rcp / div_scale chain)
+    float r = __uint_as_float(0x7EF311C3u - __float_as_uint(mx));
+    float e = __builtin_fmaf(-mx, r, 1.0f);
+    r = __builtin_fmaf(r, e, r);
+    e = __builtin_fmaf(-mx, r, 1.0f);
+    r = __builtin_fmaf(r, e, r);
+    e = __builtin_fmaf(-mx, r, 1.0f);
+    r = __builtin_fmaf(r, e, r);
+    float a = mn * r;
+#endif
     float s = a * a;
     float p = -0x1.8ba68ap-10f;
     p = __builtin_fmaf(p, s, 0x1.398008p-7f);
@@ -176,11 +192,11 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     p = __builtin_fmaf(p, s, 0x1.9986ecp-3f);
     p = __builtin_fmaf(p, s, -0x1.5554eep-2f);
     p = __builtin_fmaf(p, s, 0x1.000000p+0f);
-    float r = a * p;
-    if (ay > ax) r = kHalfPi - r;
-    if (x < 0.0f) r = kPi - r;
-    if (y < 0.0f) r = -r;
-    return (mx == 0.0f) ? 0.0f : r;  // phase of an exactly-zero bin := +0
+    float rr = a * p;
+    if (ay > ax) rr = kHalfPi - rr;
+    if (x < 0.0f) rr = kPi - rr;
+    if (y < 0.0f) rr = -rr;
+    return (mx == 0.0f) ? 0.0f : rr;  // phase of an exactly-zero bin := +0
 }
 
 // sin/cos for the bounded phases of the synthesis (|x| < 2^10): Cody-Waite reduction by

@@ -389,6 +389,9 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
+#ifndef PV_NT_OUT
+#define PV_NT_OUT 1  // non-temporal output stores in the synthesis (-0.5 %)
+#endif
 #ifndef PV_REV_ACC
 #define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
 #endif
@@ -519,7 +522,11 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
         for (int d = 0; d < D; ++d) {
             const long long gp = pb + 128 * d;
             if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
+#if PV_NT_OUT
+                __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
+#else
                 *reinterpret_cast<float2*>(outc + gp) = acc[d];
+#endif
             } else {
                 if (gp < p.out_len) outc[gp] = acc[d].x;
                 if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
