@@ -87,6 +87,19 @@ __device__ __forceinline__ f2v pk_lo_hi(f2v a, f2v b) {
     return r;
 }
 
+// top + (bot.y, -bot.x) [NEG = false] or top - (bot.y, -bot.x) = top + (-bot.y, bot.x)
+// [NEG = true]: the -i (or +i) butterfly of stage Ns = 2 with the swap and sign in the
+// VOP3P modifiers; each lane op is the single rounding of the scalar form.
+template <bool NEG>
+__device__ __forceinline__ f2v pk_add_swp(f2v top, f2v bot) {
+    f2v r;
+    if constexpr (!NEG)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(top), "v"(bot));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(top), "v"(bot));
+    return r;
+}
+
 // LDS loads the compiler must not pair into ds_read2_b32/_b64: a paired read costs 4x the
 // LDS cycles of the same bytes as ds_read_b64 (MI355X_MICROARCH.md §LDS).  Volatile
 // accesses are never merged; they still schedule freely against non-volatile code.
@@ -298,29 +311,42 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
     for (int g = 0; g < NG; ++g) {
         const int j = lane + 64 * g;
         const int jm = j & (S - 1);
-        float2 a[R];
+        // the stages run on native 2-vectors (64-bit register pairs), so the packed
+        // operations need no register moves to assemble their operands
+        f2v a[R];
 #pragma unroll
-        for (int q = 0; q < R; ++q) a[q] = v[g * R + q];
+        for (int q = 0; q < R; ++q) a[q] = f2v{v[g * R + q].x, v[g * R + q].y};
 #pragma unroll
         for (int st = 0; st < r; ++st) {
             const int Ns = S << st;
-            float2 b[R];
+            f2v b[R];
 #pragma unroll
             for (int s = 0; s < R / 2; ++s) {
                 const int br = bitrevc(s & ((1 << st) - 1), st);
                 // pass 0: jm = 0, S = 1: compile-time index into the hoisted tw0 (SGPRs)
                 // packed (v_pk_*) form of cmul + butterfly, same roundings as cmul();
                 // INV multiplies by conj(w)
-                const f2v top = f2v{a[s].x, a[s].y};
-                const f2v bot = f2v{a[s + R / 2].x, a[s + R / 2].y};
+                const f2v top = a[s];
+                const f2v bot = a[s + R / 2];
+                if (P == 0 && Ns == 2 && br != 0) {  // compile-time in pass 0
+                    // W = exactly -i (+i when INV): top +- (bot.y, -bot.x) as two packed adds
+                    // whose op_sel / neg modifiers swap and negate bot (no register moves)
+                    if constexpr (!INV) {
+                        b[2 * s] = pk_add_swp<false>(top, bot);
+                        b[2 * s + 1] = pk_add_swp<true>(top, bot);
+                    } else {
+                        b[2 * s] = pk_add_swp<true>(top, bot);
+                        b[2 * s + 1] = pk_add_swp<false>(top, bot);
+                    }
+                    continue;
+                }
                 f2v t;
-                if (Ns == 1) {
+                if (Ns == 1 || (P == 0 && Ns == 2)) {
                     t = bot;  // W = 1 exactly (fp32 contract)
                 } else if (Ns == 2) {
-                    // W = 1 (idx 0) or exactly -i (idx 1; +i when INV): a swap and a sign
+                    // later pass (L = 128): W = 1 or exactly -i (+i when INV) by lane
                     const f2v r = INV ? f2v{-bot.y, bot.x} : f2v{bot.y, -bot.x};
-                    const int idx = (P == 0) ? br : jm;
-                    t = (idx != 0) ? r : bot;
+                    t = (jm != 0) ? r : bot;
                 } else if constexpr (P == 0) {
                     const float2 w = tw0[(Ns - 1) + br];
                     t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
@@ -328,15 +354,14 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                     const float2 w = lds_ld(&tw[(Ns - 1) + jm + S * br]);
                     t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
                 }
-                const f2v u0 = top + t, u1 = top - t;
-                b[2 * s] = make_float2(u0.x, u0.y);
-                b[2 * s + 1] = make_float2(u1.x, u1.y);
+                b[2 * s] = top + t;
+                b[2 * s + 1] = top - t;
             }
 #pragma unroll
             for (int q = 0; q < R; ++q) a[q] = b[q];
         }
 #pragma unroll
-        for (int q = 0; q < R; ++q) v[g * R + q] = a[q];
+        for (int q = 0; q < R; ++q) v[g * R + q] = make_float2(a[q].x, a[q].y);
     }
 }
 
