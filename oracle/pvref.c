@@ -80,7 +80,9 @@ float pvr_atan2f(float y, float x) {
     float ax = fabsf(x), ay = fabsf(y);
     float mx = (ax > ay) ? ax : ay;
     float mn = (ax > ay) ? ay : ax;
-    if (mx == 0.0f) return 0.0f; /* phase of an exactly-zero bin is defined as +0 */
+    /* mx floored at FLT_MIN: an all-zero bin gets a = 0 and the phase +-0 (the sign of
+     * y), without a special case */
+    if (mx < 0x1p-126f) mx = 0x1p-126f;
     /* a = mn / mx without a division: reciprocal of mx from an integer seed (relative
      * error <= 5.1e-2) and three Newton steps e = 1 - mx r, r += r e (fmaf), then one
      * product; <= 6e-8 relative for normal mx (audio spectra are far from the fp32
@@ -103,8 +105,7 @@ float pvr_atan2f(float y, float x) {
     float r = a * p;
     if (ay > ax) r = PVR_HALF_PI_F - r;
     if (x < 0.0f) r = PVR_PI_F - r;
-    if (y < 0.0f) r = -r;
-    return r;
+    return copysignf(r, y); /* r >= 0: the sign of y (y = -0 gives -r, like C atan2) */
 }
 
 static inline pvr_c32 cmul_c(pvr_c32 b, pvr_c32 w) {

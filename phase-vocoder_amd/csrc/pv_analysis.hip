@@ -125,9 +125,15 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
 #else
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
 #endif
-                    const int m = unwrap_count(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
-                    if (u == 0 && rec != nullptr && (i < E || lane == 0)) rec[BP + k] = m;
-                    sacc[i] += (u == 0) ? 0 : m;
+                    // m = -mr; the run's first decision is the record's m0, not part of S:
+                    // it is subtracted like every other and added back in the (wave-
+                    // uniform, once per run) u == 0 branch
+                    const float mr = unwrap_round(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
+                    sacc[i] += mr;
+                    if (u == 0) {
+                        sacc[i] -= mr;
+                        if (rec != nullptr && (i < E || lane == 0)) rec[BP + k] = -(int)mr;
+                    }
                 }
                 phprev[i] = ph;
             }
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
         window(xr, z);
         frame(u, z, std::false_type{});
     }
-    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = sacc[i]; })
+    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = -(int)sacc[i]; })
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT

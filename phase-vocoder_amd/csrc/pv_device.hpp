@@ -167,19 +167,17 @@ __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
 #define PV_ATAN_IEEE_DIV 0  // must match the oracle's contract (it uses the division-free form)
 #endif
 // atan2 of the contract (oracle pvr_atan2f); atan(a) = a*P(a^2), |err| <= 2.7e-7 rad.
+// Zero bins: +-0 (the sign of y); y = -0 gives -phase like C's atan2.
 __device__ __forceinline__ float atan2_pv(float y, float x) {
     float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
     // max/min of |x|, |y| as single instructions with abs modifiers (fmaxf/fminf make
     // the compiler canonicalise operands it cannot prove canonical, e.g. asm results);
     // identical values for non-NaN inputs
-#ifdef PV_ATAN_FMAX
-    float mx = __builtin_fmaxf(ax, ay);
-    float mn = __builtin_fminf(ax, ay);
-#else
+// mx is floored at FLT_MIN (contract): an all-zero bin gets a = 0 and phase +-0 with
+    // no special case
     float mx, mn;
-    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(mx) : "v"(x), "v"(y));
+    asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(mx) : "v"(x), "v"(y), "s"(0x1p-126f));
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
-#endif
 #if PV_ATAN_IEEE_DIV
     float a = mn / mx;  // IEEE division (-fhip-fp32-correctly-rounded-divide-sqrt)
 #else
@@ -208,8 +206,7 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     float rr = a * p;
     if (ay > ax) rr = kHalfPi - rr;
     if (x < 0.0f) rr = kPi - rr;
-    if (y < 0.0f) rr = -rr;
-    return (mx == 0.0f) ? 0.0f : rr;  // phase of an exactly-zero bin := +0
+    return __builtin_copysignf(rr, y);  // rr >= 0 here: the sign of y (v_bfi_b32)
 }
 
 // sin/cos for the bounded phases of the synthesis (|x| < 2^10): Cody-Waite reduction by
@@ -261,6 +258,11 @@ __device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
 }
 
 // unwrap decision of the contract (oracle pvr_unwrap_count)
+// rint of the scaled deviation as a float: m = -unwrap_round(...) (exact small integer)
+__device__ __forceinline__ float unwrap_round(float phi, float phi_prev, float e) {
+    float d = (phi - phi_prev) - e;
+    return __builtin_rintf(d * kInv2Pi);
+}
 __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) {
     float d = (phi - phi_prev) - e;
     float q = d * kInv2Pi;
