@@ -141,14 +141,21 @@ struct SynLds {
 // holds (p j_k mod q) / q as floats; every value is a multiple of 1/q below 2^12, so all of
 // it is exact in fp32 and equals the integer path's offset up to whole revolutions (which
 // sin/cos ignore), for 3 VALU operations per bin less.
-template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+// hook(): called once the spectrum row sv has been consumed (before the inverse real-FFT
+// pre-step) — the batched kernel issues the next row's loads there into the same registers.
+template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false,
+          typename Hook = NoHook>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
                                             const SynLds& tb, const float2 (&tw0)[Geo<L>::E],
                                             float2* tile, int lane, float2 (&z)[Geo<L>::E],
                                             const float (&ekr)[Geo<L>::E + 1],
-                                            const unsigned (&jkr)[Geo<L>::E + 1]) {
+                                            const unsigned (&jkr)[Geo<L>::E + 1],
+                                            const Hook& hook = Hook{}) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int B = L + 1;
@@ -255,6 +262,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             Yr[i] = y;
         })
     }
+    hook();
     // inverse real-FFT pre-step: Z[i] = Fe + i Fo, pass-0 layout i = lane + 64 q, from
     // A = Y[i] (this lane's register q) and B = Y[L - i].  For lane l >= 1, bin L - i =
     // (64 - l) + 64 (E - 1 - q) is register E-1-q of lane 64 - l: a lane reversal by

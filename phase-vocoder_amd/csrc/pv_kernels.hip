@@ -129,6 +129,9 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 #ifndef PV_REV_ACC
 #define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
 #endif
+#ifndef PV_SYN_1BUF
+#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame
+#endif
 #ifndef PV_SYN_KREG
 #define PV_SYN_KREG 0  // measured: no gain over the LDS reads
 #endif
@@ -235,6 +238,10 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
         synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
     };
+    [[maybe_unused]] auto synth_h = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hook) {
+        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook);
+    };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
     auto ola_regs = [&](const float2 (&z)[E]) {
@@ -288,6 +295,24 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
             flush_regs(u, std::true_type{});  // exactly D stores
         };
         auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
+#if PV_SYN_1BUF
+        // one row buffer: row u+1 is loaded into it once frame u's phase stage has
+        // consumed it (synth_frame hook), then the pre-step, FFT and overlap-add run
+        // while it is in flight: 18 VGPRs fewer than two buffers
+        f2v row[E + 1];
+        gload_row<E>(row, rowp(0) + lane, rowp(0) + L);
+        vm_wait<0>(row);
+        for (int u = 0; u < p.F; ++u) {
+            float2 sv[E + 1];
+#pragma unroll
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
+            float2 z[E];
+            synth_h(u, t0 + u, sv, z, [&] { gload_row<E>(row, rowp(u + 1) + lane, rowp(u + 1) + L); });
+            ola_regs(z);
+            flush_regs(u, std::true_type{});  // exactly D stores
+            vm_wait<D>(row);
+        }
+#else
         f2v ra[E + 1], rb[E + 1];
         gload_row<E>(ra, rowp(0) + lane, rowp(0) + L);
         vm_wait<0>(ra);
@@ -299,6 +324,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
             step(u + 1, rb);
             vm_wait<D>(ra);
         }
+#endif
     } else {
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
         if (nfr > 0) {
