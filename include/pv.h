@@ -84,7 +84,9 @@ typedef struct pv_info {
     int n_samps, hop, out_hop;
     int spec_bins;      /* bins written per frame: N/2+1 (STANDARD) or 2N (REF_COMPAT)  */
     int spec_stride;    /* pv_float2 elements between consecutive frames of a channel   */
-    int frames_per_run; /* frames per workgroup run                      */
+    int frames_per_run; /* frames per wave run; chosen from           */
+                        /* max_channels x max_frames, or the environment variable       */
+                        /* PV_RUN_FRAMES (even, 8..256) read by pv_create               */
     int mode, effect;
     float scale;
 } pv_info;
