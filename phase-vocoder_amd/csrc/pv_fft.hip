@@ -7,11 +7,16 @@
 //   N in [128, 2048]: one transform per wavefront, the register-blocked Stockham engine of
 //     the phase-vocoder kernels (fft_run, pv_device.hpp): the same radix-2 butterflies
 //     with table twiddles, log2(N/64) stages per register pass, an LDS exchange per pass.
-//   N in [2, 64]: one transform per wavefront, lanes hold points, one radix-2 stage per
-//     LDS round (the reference's FftIteration, in LDS instead of global memory).
+//   N in [2, 64]: one transform per LANE, every stage in registers (k_fft_reg); the
+//     per-stage LDS form (the reference's FftIteration in LDS, one transform per wave)
+//     remains for buffers that are not 16-byte aligned.
 // Unnormalised in both directions, like the reference (GPU_FFT applies no 1/N).
 #include "pv_device.hpp"
 #include "pv_kernels.h"
+
+#ifndef PV_FFT_SMALL_LDS
+#define PV_FFT_SMALL_LDS 0  // 1: the per-stage LDS kernel for N <= 64 (previous form)
+#endif
 
 namespace pv {
 
@@ -79,6 +84,65 @@ __global__ __launch_bounds__(256) void k_fft_small(const float2* __restrict__ in
     if (lane < n) out[b * n + lane] = x[lane];
 }
 
+// N <= 64, register form: one transform per LANE, all log2 N radix-2 Stockham stages in
+// registers with compile-time indices (the twiddle of every butterfly is a wave-uniform
+// table entry -> scalar loads), W = 1 / exactly -i in the first two stages as in the
+// register-blocked engine; 16-byte loads and stores of the lane's contiguous transform.
+template <int N, bool INV>
+__global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, float2* out,
+                                                  const float2* __restrict__ tw, int batch) {
+    const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (b >= batch) return;
+    f2v x[N];
+    if constexpr (N == 2) {
+        const float2 a0 = in[b * 2], a1 = in[b * 2 + 1];
+        x[0] = f2v{a0.x, a0.y};
+        x[1] = f2v{a1.x, a1.y};
+    } else {
+        const float4* src = reinterpret_cast<const float4*>(in + b * N);
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+            const float4 v = src[q];
+            x[2 * q] = f2v{v.x, v.y};
+            x[2 * q + 1] = f2v{v.z, v.w};
+        }
+    }
+#pragma unroll
+    for (int Ns = 1; Ns < N; Ns <<= 1) {
+        f2v y[N];
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            const int m = j & (Ns - 1);
+            const f2v v0 = x[j], v1 = x[j + N / 2];
+            const int d = (j / Ns) * 2 * Ns + m;  // expand(j, Ns, 2)
+            if (Ns == 2 && m == 1) {              // W = exactly -i (+i when INV)
+                y[d] = pk_add_swp<INV>(v0, v1);
+                y[d + Ns] = pk_add_swp<!INV>(v0, v1);
+                continue;
+            }
+            f2v t;
+            if (Ns <= 2) {
+                t = v1;  // W = 1
+            } else {
+                const float2 w = tw[Ns - 1 + m];
+                t = cmul_v<INV, true>(v1, f2v{w.x, w.y});
+            }
+            y[d] = v0 + t;
+            y[d + Ns] = v0 - t;
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) x[q] = y[q];
+    }
+    if constexpr (N == 2) {
+        out[b * 2] = make_float2(x[0].x, x[0].y);
+        out[b * 2 + 1] = make_float2(x[1].x, x[1].y);
+    } else {
+        float4* dst = reinterpret_cast<float4*>(out + b * N);
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) dst[q] = make_float4(x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y);
+    }
+}
+
 hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
                       hipStream_t s) {
     const dim3 grid((unsigned)((batch + 3) / 4)), block(256);
@@ -94,10 +158,29 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
         case 512: PV_FFT_L(512); break;
         case 1024: PV_FFT_L(1024); break;
         case 2048: PV_FFT_L(2048); break;
-        default:
+        default: {
             if (n < 2 || n > 64 || (n & (n - 1))) return hipErrorInvalidValue;
+#if PV_FFT_SMALL_LDS
             if (inverse) hipLaunchKernelGGL((k_fft_small<true>), grid, block, 0, s, in, out, tw, n, batch);
             else hipLaunchKernelGGL((k_fft_small<false>), grid, block, 0, s, in, out, tw, n, batch);
+#else
+            // in-place use reads each lane's transform completely before writing it: safe;
+            // 16-byte vector access needs 16-byte aligned buffers (n >= 4)
+            if (n >= 4 && ((((uintptr_t)in) | ((uintptr_t)out)) & 15)) {
+                if (inverse) hipLaunchKernelGGL((k_fft_small<true>), grid, block, 0, s, in, out, tw, n, batch);
+                else hipLaunchKernelGGL((k_fft_small<false>), grid, block, 0, s, in, out, tw, n, batch);
+                break;
+            }
+            const dim3 g2((unsigned)((batch + 255) / 256));
+#define PV_FFT_R(NN_)                                                                              \
+    case NN_:                                                                                      \
+        if (inverse) hipLaunchKernelGGL((k_fft_reg<NN_, true>), g2, block, 0, s, in, out, tw, batch); \
+        else hipLaunchKernelGGL((k_fft_reg<NN_, false>), g2, block, 0, s, in, out, tw, batch);       \
+        break;
+            switch (n) { PV_FFT_R(2) PV_FFT_R(4) PV_FFT_R(8) PV_FFT_R(16) PV_FFT_R(32) PV_FFT_R(64) }
+#undef PV_FFT_R
+#endif
+        }
     }
 #undef PV_FFT_L
     return hipGetLastError();
