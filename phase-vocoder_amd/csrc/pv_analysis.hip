@@ -18,6 +18,9 @@
 #if PV_SPLIT2X && PV_PK_SPLIT
 #error "PV_SPLIT2X is implemented for the scalar real split only"
 #endif
+#ifndef PV_BINL_FULL
+#define PV_BINL_FULL 0  // bin L as a whole 64-byte segment with the row padding (measured: no gain)
+#endif
 #ifndef PV_ANA_SHIFT
 #define PV_ANA_SHIFT 1  // shifted-register input when hop = 128 D (k_std_analysis<L, false, D>)
 #endif
@@ -118,9 +121,19 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
                     float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                     if (PV_SPLIT2X) mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
                     // bin L (i = E) has the same value and address on every lane
-#if PV_NT_SPEC
+#if PV_NT_SPEC && PV_BINL_FULL
                     // non-temporal: the rows are read back by another launch, long after
-                    // they would have left L2 (measured: analysis -7 %)
+                    // they would have left L2 (measured: analysis -7 %).  Bin L goes out
+                    // with the row's 7 padding bins (zeros) as one whole 64-byte segment
+                    // from lanes 0..7 instead of an 8-byte partial write (stride = L + 8).
+                    if (i == E) {
+                        if (lane < 8)
+                            __builtin_nontemporal_store(lane == 0 ? f2v{mag, ph} : f2v{0.0f, 0.0f},
+                                                        reinterpret_cast<f2v*>(&srow[L]));
+                    } else {
+                        __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
+                    }
+#elif PV_NT_SPEC
                     __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
 #else
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);

@@ -64,23 +64,25 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
     const bool on = k <= p.L;
     const int* rs = p.runsum + (long long)c * p.nruns * 2 * BP + (on ? k : 0);
     int* cr = p.carry + (long long)c * p.nruns * BP + (on ? k : 0);
-    int T = 0;
-    int run = r0;
-    for (; run + 4 <= r1; run += 4) {
-        int a[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            a[2 * j] = rs[(long long)(run + j) * 2 * BP];
-            a[2 * j + 1] = rs[(long long)(run + j) * 2 * BP + BP];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) T += a[j];
-    }
-    for (; run < r1; ++run) T += rs[(long long)run * 2 * BP] + rs[(long long)run * 2 * BP + BP];
-    tot[sg][lane] = T;
-    __syncthreads();
     int M = 0;
-    for (int j = 0; j < sg; ++j) M += tot[j][lane];
+    int run = r0;
+    if constexpr (SEG > 1) {  // pass 1 only feeds the other segments' offsets
+        int T = 0;
+        for (; run + 4 <= r1; run += 4) {
+            int a[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[2 * j] = rs[(long long)(run + j) * 2 * BP];
+                a[2 * j + 1] = rs[(long long)(run + j) * 2 * BP + BP];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) T += a[j];
+        }
+        for (; run < r1; ++run) T += rs[(long long)run * 2 * BP] + rs[(long long)run * 2 * BP + BP];
+        tot[sg][lane] = T;
+        __syncthreads();
+        for (int j = 0; j < sg; ++j) M += tot[j][lane];
+    }
     if (!on) return;
     run = r0;
     for (; run + 4 <= r1; run += 4) {

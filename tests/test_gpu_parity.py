@@ -188,6 +188,23 @@ def test_std_process_parity_geometries(cuda, N, hop_div, effect, scale):
     assert rms(out.cpu().numpy()[0], ref) <= RMS_TOL
 
 
+@pytest.mark.parametrize("C", [1, 32])
+def test_long_streams_segmented_carry(cuda, C):
+    """Long streams with few channels take the segmented unwrap-count scans (k_carry with
+    16 run segments per 64 bins at C = 1, 4 at C = 32): integer, so the split cannot change
+    a bit; checked end to end against the oracle (stretch 0.5 needs the carries, q = 2)."""
+    N, hop_div, n = 1024, 4, 780000  # ~3050 frames per channel
+    xs = np.stack([synth(n, 900 + c) for c in range(C)])
+    pv = PhaseVocoder(N, TIME_SHIFT, 0.5, hop_div, mode=STANDARD, max_channels=C, max_frames=3100)
+    nruns = -(-pv.num_frames(n) // pv.frames_per_run)
+    assert nruns >= 64  # the segmented scans only run for >= 64 runs
+    out, _ = pv.process(to_dev(xs))
+    g = out.cpu().numpy()
+    ref, _ = pvref.std_process_batch(xs, N, hop_div, ord("t"), 0.5)
+    for c in range(C):
+        assert rms(g[c], ref[c]) <= RMS_TOL, f"C={C} ch{c}"
+
+
 @pytest.mark.parametrize("mode", [STANDARD, REF_COMPAT])
 def test_odd_output_stride(cuda, mode):
     """out rows at an odd float stride: the vectorised stores must fall back to scalar."""
