@@ -81,8 +81,8 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
     float phprev[E + 1];
-    int sacc[E + 1];
-    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0; })
+    float sacc[E + 1];  // -(sum of the run's decisions): exact small integers in fp32
+    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0.0f; })
     // run record {S, m0}: m0 (the decision of the run's first frame) is stored as soon as
     // it is known, S after the loop
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * 2 * BP : nullptr;
