@@ -195,7 +195,9 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            traffic = tj.get(dom, {}).get("bytes_per_launch")
+            # measured on one workload (config 3 by default): no number for the others
+            if tj.get("_workload", "c3") == wl:
+                traffic = tj.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}

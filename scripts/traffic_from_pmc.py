@@ -54,5 +54,6 @@ for k, cs in per.items():
     res[name if name not in res else k] = {"kernel": k, "read_bytes_per_launch": rd,
                                            "write_bytes_per_launch": wr,
                                            "bytes_per_launch": rd + wr}
+res["_workload"] = os.environ.get("PV_TRAFFIC_WORKLOAD", "c3")  # what prof_kernels.py ran
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
