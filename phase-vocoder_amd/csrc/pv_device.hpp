@@ -111,6 +111,10 @@ __device__ __forceinline__ float2 lds_ld(const float2* p) {
 __device__ __forceinline__ float lds_ld(const float* p) { return *(const volatile PV_LDS float*)(p); }
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return *(const volatile PV_LDS unsigned*)(p); }
 __device__ __forceinline__ int lds_ld(const int* p) { return *(const volatile PV_LDS int*)(p); }
+typedef int i2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i2v lds_ld2i(const int* p) {  // 8-byte aligned pair
+    return *(const volatile PV_LDS i2v*)(p);
+}
 
 // ---------------------------------------------------------------------------
 // Self-tracked prefetch.  vmcnt counts loads and stores together in issue order and the

@@ -123,7 +123,7 @@ struct SynLds {
     const float2* twsl;   // e^{-2 pi i k/N}, k <= L
     const float* ekl;     // expected advance e_k (STANDARD)
     const unsigned* jkl;  // (p j_k) mod q (STANDARD)
-    const int* srcl;      // pitch map: first source bin [B], source count [B] (MODE 2)
+    const int* srcl;      // pitch map: {first source bin, source count} per bin [B] (MODE 2)
 };
 
 // One synthesis frame from the spectrum row sv (mag, phase of the lane's bins k = lane +
@@ -226,13 +226,15 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
             wave_lds_sync();
             PV_FOR_BINS(E, lane, {
-                const int s = srcl[k];
-                float ms = 0.0f, pc = 0.0f;
-                if (s >= 0) {
-                    const int cnt = srcl[B + k];
-                    pc = tile[G_::pad(s)].y;
-                    for (int qq = 0; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
-                }
+                // {first source, count} in one 8-byte read; the first source's {mag, phase}
+                // in one read, without a branch (zero when no source maps here); more
+                // sources (ratios < 1) are summed in order like the oracle
+                const i2v sc = lds_ld2i(&srcl[2 * k]);
+                const int s = sc.x, cnt = sc.y;
+                const float2 f = lds_ld(&tile[G_::pad(s >= 0 ? s : 0)]);
+                float ms = (s >= 0) ? f.x : 0.0f;
+                const float pc = (s >= 0) ? f.y : 0.0f;
+                for (int qq = 1; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
                 float sn, cs;
                 sincos_rev(pc, &sn, &cs);
                 Y[i] = make_float2(ms * cs, ms * sn);

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
             ekl[i] = p.ek[i];
             // RACC: (p j_k mod q) / q as a float (exact: q <= 4096)
             jkl[i] = RACC ? __float_as_uint((float)p.jk_mod[i] * p.inv_q) : p.jk_mod[i];
-            if (MODE == 2) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
+            if (MODE == 2) { srcl[2 * i] = p.src_first[i]; srcl[2 * i + 1] = p.src_cnt[i]; }
         }
     }
     float* ring = rings + w * N;  // ROLA: the run's tail, written after the frame loop

@@ -36,8 +36,9 @@ struct RtGeo {
     static constexpr int O_GAIN = O_WIN + N;                // N
     static constexpr int O_EK = O_GAIN + N;                 // B (+3)
     static constexpr int O_JK = O_EK + (B + 3);             // B (+3)
-    static constexpr int O_SRC = O_JK + (B + 3);            // 2B (+2)
+    static constexpr int O_SRC = O_JK + (B + 3);            // 2B (+2), {first, count} pairs
     static constexpr int O_BUF = O_SRC + (2 * B + 2);       // W x N input window
+    static_assert(O_SRC % 2 == 0, "pitch map pairs are read as 8-byte words");
     static constexpr int O_OLA = O_BUF + W * N;             // W x N overlap accumulator
     static constexpr int FLOATS = O_OLA + W * N;
     static constexpr size_t BYTES = sizeof(float) * FLOATS;
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
         twsl[i] = p.tws[i];
         ekl[i] = p.ek[i];
         jkl[i] = p.jk_mod[i];
-        if (MODE == 2) { srcl[i] = p.src_first[i]; srcl[B + i] = p.src_cnt[i]; }
+        if (MODE == 2) { srcl[2 * i] = p.src_first[i]; srcl[2 * i + 1] = p.src_cnt[i]; }
     }
     for (int i = tid; i < N; i += 64 * W) { winl[i] = p.win[i]; gainl[i] = p.gain[i]; }
     __syncthreads();
