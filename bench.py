@@ -200,6 +200,19 @@ def main():
                 traffic = tj.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
+    # the box's measured HBM ceilings (scripts/bw_probe.hip -> profiles/r01_bw_probe.jsonl):
+    # the 8 TB/s peak is the spec figure; copy streams reach ~4.8 TB/s on MI355X
+    ceiling = None
+    probe = os.path.join(ROOT, "profiles", "r01_bw_probe.jsonl")
+    if os.path.exists(probe):
+        try:
+            rows = {d["probe"]: d["GBps"] for d in map(json.loads, open(probe)) if d}
+            copy = max(v for k, v in rows.items() if k.startswith("copy"))
+            ceiling = {"copy_GBps": copy, "frac_of_copy": achieved / copy,
+                       "traffic_frac_of_copy": (traffic / (avg_ms * 1e-3) / 1e9 / copy) if traffic else None,
+                       "source": "profiles/r01_bw_probe.jsonl"}
+        except Exception:
+            ceiling = None
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}
     path_bytes = (4 * hop_a + 4 * hop_s + 2 * 8 * B) * C * frames * world * args.steps
 
@@ -224,6 +237,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
+            "measured_ceiling": ceiling,
             "kernels": kernels,
             "tables_broadcast": tables,
             "cpu_baseline": cpu,
