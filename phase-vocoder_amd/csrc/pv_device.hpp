@@ -124,13 +124,17 @@ __device__ __forceinline__ i2v lds_ld2i(const int* p) {  // 8-byte aligned pair
 // exactly K unconditional stores, then vm_wait<K>, all within one loop trip (so the
 // registers are never copied or spilled while the loads are in flight; check
 // "VGPRs Spill: 0" in the resource-usage report).
-template <int E>
+template <int E, bool NT = false>
 __device__ __forceinline__ void gload_pairs(f2v (&xr)[E], const float* src) {
 #pragma unroll
     for (int q = 0; q < E; ++q) {
         const float* pq = src + 1024 * (q >> 3);  // 13-bit signed immediate offsets
-        asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
-                     : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+        if constexpr (NT)
+            asm volatile("global_load_dwordx2 %0, %1, off offset:%2 nt"
+                         : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+        else
+            asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
+                         : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
 // the last D pairs of gload_pairs<E>: registers q = E-D .. E-1
@@ -145,13 +149,20 @@ __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
                      : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
+#ifndef PV_NT_ROWS
+#define PV_NT_ROWS 1  // measured +0.4 % (config 3)
+#endif
 // one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and bin L (the
 // same address on every lane) from rowL
 template <int E>
 __device__ __forceinline__ void gload_row(f2v (&v)[E + 1], const float2* rowlane, const float2* rowL) {
     f2v (&head)[E] = *reinterpret_cast<f2v(*)[E]>(&v[0]);
-    gload_pairs<E>(head, reinterpret_cast<const float*>(rowlane));
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");
+    // rows are read exactly once: PV_NT_ROWS streams them past the caches
+    gload_pairs<E, (bool)PV_NT_ROWS>(head, reinterpret_cast<const float*>(rowlane));
+    if constexpr ((bool)PV_NT_ROWS)
+        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v[E]) : "v"(rowL) : "memory");
+    else
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");
 }
 template <int K, int E>
 __device__ __forceinline__ void vm_wait(f2v (&xr)[E]) {
