@@ -137,6 +137,9 @@ __device__ __forceinline__ void gload_pairs(f2v (&xr)[E], const float* src) {
                          : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
+#ifndef PV_NT_INPUT
+#define PV_NT_INPUT 0  // non-temporal input loads: measured +0.1 % (noise), off
+#endif
 // the last D pairs of gload_pairs<E>: registers q = E-D .. E-1
 template <int D, int E>
 __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
@@ -145,8 +148,12 @@ __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
         constexpr int Q0 = E - D;
         const int q = Q0 + j;
         const float* pq = src + 1024 * (q >> 3);
-        asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
-                     : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+        if constexpr ((bool)PV_NT_INPUT)  // each sample pair is read once here
+            asm volatile("global_load_dwordx2 %0, %1, off offset:%2 nt"
+                         : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+        else
+            asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
+                         : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
 #ifndef PV_NT_ROWS
