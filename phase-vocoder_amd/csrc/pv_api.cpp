@@ -854,6 +854,9 @@ pv_status pv_rt_push(pv_rt* rt, const float* in, long long ldi, int nframes, flo
     return PV_OK;
 }
 
+#ifndef PV_RT_ZERO_COPY
+#define PV_RT_ZERO_COPY 1
+#endif
 pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     if (!rt) return fail(PV_ERR_ARG, "null rt");
     if (nframes <= 0) return fail(PV_ERR_ARG, "nframes must be > 0");
@@ -863,24 +866,39 @@ pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     if (!rt->g_stream) PV_HIP(hipStreamCreateWithFlags(&rt->g_stream, hipStreamNonBlocking));
     const size_t C = (size_t)rt->channels;
     const size_t ni = (size_t)nframes * h->hop, no = (size_t)nframes * h->hs;
-    PV_HIP(hipHostMalloc((void**)&rt->h_in, sizeof(float) * C * ni, hipHostMallocDefault));
-    PV_HIP(hipHostMalloc((void**)&rt->h_out, sizeof(float) * C * no, hipHostMallocDefault));
-    PV_HIP(hipMalloc((void**)&rt->d_in, sizeof(float) * C * ni));
-    PV_HIP(hipMalloc((void**)&rt->d_out, sizeof(float) * C * no));
+    // pinned, device-mapped host buffers: the captured kernel reads the callback's input
+    // and writes its output in place over the bus (zero-copy: the graph is one kernel
+    // node, no copy nodes); if the runtime cannot map them, the graph copies H2D / D2H
+    // around the kernel instead (PV_RT_ZERO_COPY=0 forces that form)
+    PV_HIP(hipHostMalloc((void**)&rt->h_in, sizeof(float) * C * ni, hipHostMallocMapped));
+    PV_HIP(hipHostMalloc((void**)&rt->h_out, sizeof(float) * C * no, hipHostMallocMapped));
     std::memset(rt->h_in, 0, sizeof(float) * C * ni);
     std::memset(rt->h_out, 0, sizeof(float) * C * no);
+    float *m_in = nullptr, *m_out = nullptr;
+    bool zero_copy = PV_RT_ZERO_COPY &&
+                     hipHostGetDevicePointer((void**)&m_in, rt->h_in, 0) == hipSuccess &&
+                     hipHostGetDevicePointer((void**)&m_out, rt->h_out, 0) == hipSuccess && m_in && m_out;
+    if (!zero_copy) {
+        (void)hipGetLastError();
+        PV_HIP(hipMalloc((void**)&rt->d_in, sizeof(float) * C * ni));
+        PV_HIP(hipMalloc((void**)&rt->d_out, sizeof(float) * C * no));
+    }
     const bool was_prof = h->prof.enabled;
     h->prof.enabled = false;  // no event records inside the graph
     hipStream_t s = rt->g_stream;
     PV_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     pv_status st = PV_OK;
-    if (hipMemcpyAsync(rt->d_in, rt->h_in, sizeof(float) * C * ni, hipMemcpyHostToDevice, s) != hipSuccess)
-        st = fail(PV_ERR_HIP, "pv_rt_capture: H2D capture failed");
-    if (st == PV_OK)
-        st = pv_rt_push(rt, rt->d_in, (long long)ni, nframes, rt->d_out, (long long)no, nullptr, 0, s);
-    if (st == PV_OK &&
-        hipMemcpyAsync(rt->h_out, rt->d_out, sizeof(float) * C * no, hipMemcpyDeviceToHost, s) != hipSuccess)
-        st = fail(PV_ERR_HIP, "pv_rt_capture: D2H capture failed");
+    if (zero_copy) {
+        st = pv_rt_push(rt, m_in, (long long)ni, nframes, m_out, (long long)no, nullptr, 0, s);
+    } else {
+        if (hipMemcpyAsync(rt->d_in, rt->h_in, sizeof(float) * C * ni, hipMemcpyHostToDevice, s) != hipSuccess)
+            st = fail(PV_ERR_HIP, "pv_rt_capture: H2D capture failed");
+        if (st == PV_OK)
+            st = pv_rt_push(rt, rt->d_in, (long long)ni, nframes, rt->d_out, (long long)no, nullptr, 0, s);
+        if (st == PV_OK &&
+            hipMemcpyAsync(rt->h_out, rt->d_out, sizeof(float) * C * no, hipMemcpyDeviceToHost, s) != hipSuccess)
+            st = fail(PV_ERR_HIP, "pv_rt_capture: D2H capture failed");
+    }
     hipGraph_t graph = nullptr;
     hipError_t e = hipStreamEndCapture(s, &graph);
     h->prof.enabled = was_prof;
