@@ -11,7 +11,13 @@ ranks with no data-path collective (weak scaling).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--no-cpu]
   torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL)
 
-Rank 0 prints ONE JSON line (metric, value, roofline{...}, cpu_baseline{...}, ...).
+The synthetic channels are generated once on the host and uploaded; after the timed
+steps the whole output is checked for finiteness and 16 channels spread over the batch
+(first and last included) are compared with the CPU oracle (`rms_vs_oracle`, bar 1e-5
+RMS per sample), and the CPU baseline is timed on a bounded prefix of the same channels.
+
+Rank 0 prints ONE JSON line (metric, value, roofline{...}, rms_vs_oracle{...},
+cpu_baseline{...}, ...).
 """
 from __future__ import annotations
 
@@ -32,69 +38,100 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SR = 44100
 
 
-def synth_channels(torch, C, n, seed0, device):
-    """configs 2-4 generator (BASELINE.md §2): 3 sines f~U[55,4000] Hz, a=0.1, random
-    phase, + U(+-1e-3) noise, seed = seed0 + channel.  Built on the device (plumbing)."""
-    t = torch.arange(n, dtype=torch.float64, device=device) / SR
-    x = torch.empty((C, n), dtype=torch.float32, device=device)
-    for c in range(C):
-        rng = np.random.default_rng(seed0 + c)
-        f = rng.uniform(55, 4000, 3)
-        ph = rng.uniform(0, 2 * np.pi, 3)
-        acc = torch.zeros(n, dtype=torch.float64, device=device)
-        for i in range(3):
-            acc += 0.1 * torch.sin(2 * np.pi * float(f[i]) * t + float(ph[i]))
-        g = torch.Generator(device=device).manual_seed(seed0 + c)
-        acc += (torch.rand(n, dtype=torch.float64, device=device, generator=g) * 2 - 1) * 1e-3
-        x[c] = acc.to(torch.float32)
-    return x
+def cpu_share():
+    """(threads the CPU legs use, CPUs in this process's affinity mask).  On the GPU pool
+    `nproc`/os.cpu_count() show the whole machine while one GPU's share is 16 CPUs
+    (OMP_NUM_THREADS is set to it there), so the share is min(affinity, OMP_NUM_THREADS);
+    PV_CPU_THREADS overrides."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = min(aff, omp) if omp > 0 else aff
+    return int(os.environ.get("PV_CPU_THREADS", "0") or 0) or share, aff
 
 
-def synth_channels_np(C, n, seed0):
+def _synth_one(c, n, seed0, out):
     t = np.arange(n) / SR
+    rng = np.random.default_rng(seed0 + c)
+    f = rng.uniform(55, 4000, 3)
+    ph = rng.uniform(0, 2 * np.pi, 3)
+    acc = sum(0.1 * np.sin(2 * np.pi * f[i] * t + ph[i]) for i in range(3))
+    acc = acc + rng.uniform(-1e-3, 1e-3, n)
+    out[c] = acc.astype(np.float32)
+
+
+def synth_channels_np(C, n, seed0, threads=1):
+    """configs 2-4 generator (BASELINE.md §2): 3 sines f~U[55,4000] Hz, a=0.1, random
+    phase, + U(+-1e-3) noise, seed = seed0 + channel.  Built once on the host: the GPU
+    batch, the CPU baseline and the oracle check all read this same array."""
     out = np.empty((C, n), np.float32)
-    for c in range(C):
-        rng = np.random.default_rng(seed0 + c)
-        f = rng.uniform(55, 4000, 3)
-        ph = rng.uniform(0, 2 * np.pi, 3)
-        acc = sum(0.1 * np.sin(2 * np.pi * f[i] * t + ph[i]) for i in range(3))
-        acc = acc + rng.uniform(-1e-3, 1e-3, n)
-        out[c] = acc.astype(np.float32)
+    if threads <= 1 or C == 1:
+        for c in range(C):
+            _synth_one(c, n, seed0, out)
+    else:
+        from concurrent.futures import ThreadPoolExecutor  # numpy ufuncs release the GIL
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda c: _synth_one(c, n, seed0, out), range(C)))
     return out
 
 
-def cpu_baseline(N, hop_div, effect, scale, n, target_s=10.0, single=False):
-    """The CPU oracle (oracle/pvref.c, OpenMP over channels) on a bounded sample; a single
-    stream (single=True) has no channel parallelism and runs on one core."""
+def _pvref():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pvref  # test infrastructure: used here only as the timed CPU baseline
+    import pvref  # test infrastructure: the timed CPU baseline and the checker, never the product
+    return pvref
 
-    threads = int(os.environ.get("PV_CPU_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+
+def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False):
+    """The CPU oracle (oracle/pvref.c, OpenMP over channels) timed on a bounded sample of
+    the SAME host channels the GPU processes (x: [C, n] float32).  A single stream
+    (single=True) has no channel parallelism and runs on one core."""
+    pvref = _pvref()
+    threads, aff = cpu_share()
+    C_all, n = x.shape
+    frames = pvref.num_frames(n, N // hop_div)
+    host = f"{threads} threads = this process's CPU share (affinity {aff}, machine {os.cpu_count()})"
     if single:
-        threads = 1
-        x = synth_channels_np(1, n, 20240)
-        frames = pvref.num_frames(n, N // hop_div)
         t0 = time.perf_counter()
-        _, used = pvref.std_process_batch(x, N, hop_div, effect, scale, frames, 1)
+        _, used = pvref.std_process_batch(x[:1], N, hop_div, effect, scale, frames, 1)
         dt = time.perf_counter() - t0
         return {"value": frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
-                "sample": f"the whole stream ({n} samples, {frames} frames), oracle/pvref.c, "
-                          f"{dt:.1f} s wall"}
-    frames = pvref.num_frames(n, N // hop_div)
-    probe = synth_channels_np(threads, n, 20240)
+                "sample": f"the whole stream ({n} samples, {frames} frames) on 1 core, "
+                          f"oracle/pvref.c, {dt:.1f} s wall"}
+    k = min(threads, C_all)
     t0 = time.perf_counter()
-    _, used = pvref.std_process_batch(probe, N, hop_div, effect, scale, frames, threads)
+    _, used = pvref.std_process_batch(x[:k], N, hop_div, effect, scale, frames, threads)
     dt = time.perf_counter() - t0
-    rate = threads * frames / dt
-    C = max(threads, int(rate * target_s / frames) // threads * threads)
-    C = min(C, 1024)
-    xs = synth_channels_np(C, n, 20240)
+    rate = k * frames / dt
+    C = max(k, int(rate * target_s / frames) // threads * threads)
+    C = min(C, C_all)
     t0 = time.perf_counter()
-    _, used = pvref.std_process_batch(xs, N, hop_div, effect, scale, frames, threads)
+    _, used = pvref.std_process_batch(x[:C], N, hop_div, effect, scale, frames, threads)
     dt = time.perf_counter() - t0
     return {"value": C * frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
-            "sample": f"{C} of the workload's channels x {n} samples ({C * frames} frames), "
-                      f"oracle/pvref.c fp32-contract analysis + fp64 synthesis, {dt:.1f} s wall"}
+            "sample": f"channels 0..{C - 1} of the GPU batch x {n} samples ({C * frames} frames), "
+                      f"oracle/pvref.c fp32-contract analysis + fp64 synthesis, {dt:.1f} s wall; "
+                      f"{host}"}
+
+
+def check_channels(C, k=16):
+    """k channel indices spread over the batch, first and last included."""
+    return sorted(set(int(round(v)) for v in np.linspace(0, C - 1, min(k, C))))
+
+
+def oracle_check(x, out_rows, idx, N, hop_div, effect, scale, frames, all_finite):
+    """RMS per sample of the GPU output against the oracle on the sampled channels of
+    the timed batch (BASELINE.json metric: "RMS err vs CPU ref"; bar 1e-5)."""
+    pvref = _pvref()
+    threads, _ = cpu_share()
+    ref, _ = pvref.std_process_batch(x[idx], N, hop_div, effect, scale, frames, threads)
+    got = out_rows[:, :ref.shape[1]]
+    rms = np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2, axis=1))
+    return {"max": float(rms.max()), "mean": float(rms.mean()), "tol": 1e-5,
+            "pass": bool(rms.max() <= 1e-5 and all_finite), "channels": idx,
+            "all_finite": bool(all_finite),
+            "oracle": "oracle/pvref.c pvr_std_process_batch (fp32-contract analysis, fp64 synthesis)"}
 
 
 def main():
@@ -104,7 +141,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the timed CPU baseline")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the oracle check of the timed batch (profiling passes only)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--workload", choices=["c3", "c2", "c4", "rt", "batch"], default="c3",
                     help="c3 (= batch): configs[2], the headline line (default); c2: configs[1] "
@@ -148,7 +187,11 @@ def main():
         from pvamd.dist import broadcast_tables
         same = broadcast_tables(pv, src=0)
         tables = {"bytes": int(pv.export_tables().numel()), "bit_identical_to_local": same}
-    x = synth_channels(torch, C, n, 20240 + rank * C, dev)
+    threads, _ = cpu_share()
+    t_gen = time.perf_counter()
+    x_host = synth_channels_np(C, n, 20240 + rank * C, threads)
+    x = torch.from_numpy(x_host).to(dev)
+    t_gen = time.perf_counter() - t_gen
     spec = pv.alloc_spec(C, frames)
     out = pv.alloc_out(C, frames)
     stream = torch.cuda.current_stream(dev)
@@ -214,12 +257,28 @@ def main():
         except Exception:
             ceiling = None
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}
+
+    # parity of the timed batch: every sample finite, sampled channels vs the oracle
+    check = None
+    if not args.no_check:
+        idx = check_channels(C)
+        finite = bool(torch.isfinite(out).all().item())
+        check = oracle_check(x_host, out[idx].cpu().numpy(), idx, N, hop_div, ord(effect), scale,
+                             frames, finite)
+        if world > 1:  # worst rank
+            t = torch.tensor([check["max"], check["mean"], 0.0 if check["pass"] else 1.0,
+                              0.0 if finite else 1.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            check.update(max=float(t[0]), mean=float(t[1]), ranks=world,
+                         channels=f"{len(idx)} per rank (indices as rank 0's, rank-local)")
+            check["pass"] = bool(t[2] == 0)
+            check["all_finite"] = bool(t[3] == 0)
     path_bytes = (4 * hop_a + 4 * hop_s + 2 * 8 * B) * C * frames * world * args.steps
 
     cpu = None
     if rank == 0 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(N, hop_div, ord(effect), scale, n, single=(C == 1))
+            cpu = cpu_baseline(x_host, N, hop_div, ord(effect), scale, single=(C == 1))
         except Exception as e:  # reported, never fatal for the GPU number
             cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                    "sample": f"failed: {e}"}
@@ -240,7 +299,9 @@ def main():
             "measured_ceiling": ceiling,
             "kernels": kernels,
             "tables_broadcast": tables,
+            "rms_vs_oracle": check,
             "cpu_baseline": cpu,
+            "host_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -265,7 +326,7 @@ def bench_rt(args):
     steps = args.steps if args.steps != 10 else 2000
     warm = max(args.warmup, 50)
     rt.capture(1)
-    blocks = synth_channels_np(C, hop * 64, 20240).reshape(C, 64, hop)
+    blocks = synth_channels_np(C, hop * 64, 20240, cpu_share()[0]).reshape(C, 64, hop)
     for j in range(warm):
         rt.host_in[:] = blocks[:, j % 64]
         rt.callback()

@@ -7,9 +7,15 @@
 //   CudaPhase::test_overlap_add(...)                               kernel.cu:289-298
 //   CudaPhase::timer()  PerformanceTimer (karnel/common.h:27-113) on hipEvents
 //
-// The REF_COMPAT handles behind these free functions are created on first use per
-// (N, hop) and cached for the process lifetime; `win` must be the reference's window
-// (the handle holds an identical copy), `fft` / `intermediary` are unused.
+// Every call runs the REF_COMPAT path of one frame on the legacy default stream and is
+// bracketed by timer().startGpuTimer()/endGpuTimer() like the reference, so
+// `CudaPhase::timer().getGpuElapsedTimeForPreviousOperation()` (main.cpp:240, :277) reads
+// the call's device time.  The caller's window `win` (device or managed pointer, N floats)
+// is honoured: it is handed to the handle with pv_set_window on every call, then multiplies
+// the analysis frame (kernel.cu:301) and the resynthesised frame (kernel.cu:406).  `fft` /
+// `intermediary` are unused (the window product stays on chip).  The handles behind the
+// free functions are created on first use per (N, hop, nan_faithful) and cached for the
+// process lifetime.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -17,11 +23,10 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
-#include <utility>
+#include <tuple>
 
 #include "common.h"
 #include "pv.h"
-
 
 namespace CudaPhase {
 
@@ -37,11 +42,18 @@ inline void check(pv_status st, const char* msg) {  // checkCUDAError_ (io.cpp:1
         std::exit(EXIT_FAILURE);
     }
 }
+// kernel.cu:101-109: atanf(0/0) = NaN for an all-zero bin (digital silence) poisons the
+// frame; off by default (SURVEY.md §8c deviation 4), on = the reference's behaviour
+inline int& nan_faithful_flag() {
+    static int f = 0;
+    return f;
+}
 inline pv_handle* compat_handle(int N, int hop) {
     static std::mutex mu;
-    static std::map<std::pair<int, int>, pv_handle*> cache;
+    static std::map<std::tuple<int, int, int>, pv_handle*> cache;
+    const int nf = nan_faithful_flag();
     std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find({N, hop});
+    auto it = cache.find({N, hop, nf});
     if (it != cache.end()) return it->second;
     pv_config cfg{};
     cfg.n_samps = N;
@@ -51,12 +63,13 @@ inline pv_handle* compat_handle(int N, int hop) {
     cfg.mode = PV_MODE_REF_COMPAT;
     cfg.max_channels = 1;
     cfg.max_frames = 1;
+    cfg.nan_faithful = nf;
     int dev = 0;
     (void)hipGetDevice(&dev);
     cfg.device = dev;
     pv_handle* h = nullptr;
     check(pv_create(&cfg, &h), "pv_create");
-    cache[{N, hop}] = h;
+    cache[{N, hop, nf}] = h;
     return h;
 }
 inline int spec_stride(pv_handle* h) {
@@ -66,25 +79,31 @@ inline int spec_stride(pv_handle* h) {
 }
 }  // namespace detail
 
-// kernel.cu:299-348
+// Select the reference's NaN phase for all-zero bins (kernel.cu:101-109) for later calls.
+inline void set_nan_faithful(bool on) { detail::nan_faithful_flag() = on ? 1 : 0; }
+
+// kernel.cu:299-348: output = 2N {mag, atanf(Im/Re)} of the zero-phase, zero-padded,
+// windowed frame input[0..N)
 inline void pv_analysis_CUFFT(float2* output, float2* fft, float* input, float* intermediary,
                               float* win, int N) {
     (void)fft;
     (void)intermediary;
-    (void)win;
     timer().startGpuTimer();
     pv_handle* h = detail::compat_handle(N, N / 2);
+    detail::check(pv_set_window(h, win, nullptr), "Window analysis");
     detail::check(pv_analysis(h, input, N, N, 1, 1, (pv_float2*)output, detail::spec_stride(h), nullptr),
                   "pv_analysis_CUFFT");
     timer().endGpuTimer();
 }
 
-// kernel.cu:352-432 (output = frame + backFrame[hop..N) shifted to the front)
+// kernel.cu:352-432: output[0..N) = window * shift(C2R_N(timeScale(frontFrame)) / N)
+// + backFrame[hopSize..N) shifted to the front (cudaOverlapAdd, kernel.cu:111-119).
+// frontFrame is read only here (the reference's in-place cudaTimeScale clobbers it).
 inline void resynthesis_CUFFT(float* output, float* backFrame, float2* frontFrame, float* win,
                               int N, int hopSize) {
-    (void)win;
     timer().startGpuTimer();
     pv_handle* h = detail::compat_handle(N, hopSize);
+    detail::check(pv_set_window(h, win, nullptr), "window error");
     detail::check(pv_resynthesis(h, (const pv_float2*)frontFrame, detail::spec_stride(h), 1, 1,
                                  backFrame + hopSize, N, output, N, nullptr),
                   "resynthesis_CUFFT");
@@ -106,9 +125,10 @@ inline void resynthesis(float* output, float* backFrame, float2* frontFrame, flo
 inline void test_overlap_add(float* input, float* output, float* intermediary, float* backFrame,
                              float* win, int N, int hopSize) {
     (void)intermediary;
+    timer().startGpuTimer();
     detail::check(pv_test_overlap_add(input, win, backFrame, output, N, hopSize, nullptr),
                   "test_overlap_add");
-    (void)hipStreamSynchronize(nullptr);
+    timer().endGpuTimer();
 }
 
 }  // namespace CudaPhase

@@ -1,40 +1,62 @@
 // phaseVocoder.h — header-only C++ drop-in for the reference's `class PhaseVocoder`
 // (src/phaseVocoder.h:9-139, src/phaseVocoder.cpp:20-78) on top of the libpv C-ABI
-// (include/pv.h).  Same class / enum / member / method names and argument meaning;
-// buffers are device pointers (hipMalloc or hipMallocManaged), calls are synchronous on
-// the default stream like the reference (cudaStreamSynchronize around every call,
-// phaseVocoder.cpp:28-30), and failures print and exit like checkCUDAError_
-// (src/io.cpp:115-124).
+// (include/pv.h) and the CudaPhase drop-in (include/kernel.h).  Same class / enum /
+// member / method names and argument meaning; buffers are device or managed pointers
+// (hipMalloc / hipMallocManaged); calls are synchronous on the default stream like the
+// reference (cudaStreamSynchronize around every call, phaseVocoder.cpp:28-30); failures
+// print and exit like checkCUDAError_ (src/io.cpp:115-124).
 //
-// What differs by construction: cuFFT plans, the three CUDA streams and
-// the managed-memory attach calls do not exist (the handle owns its tables); the window
-// table `imp` is a device copy of the same symmetric Hamming recipe (phaseVocoder.h:85-89).
+// Layering as in the reference: in REF_COMPAT mode the per-frame methods call
+// CudaPhase::pv_analysis_CUFFT / resynthesis_CUFFT / test_overlap_add with this->imp as
+// the window (phaseVocoder.cpp:20-76), so CudaPhase::timer() times them as main.cpp:240
+// and :277 expect.  The two constructors build the reference's two windows:
+//   PhaseVocoder(int samples)                    periodic Hann 0.5f*(1-cosf(2 pi i/N)),
+//                                                hop N/2, timeScale 1 (phaseVocoder.h:46-78)
+//   PhaseVocoder(int samples, Effect, float, int) symmetric Hamming, hop N/div
+//                                                (phaseVocoder.h:79-116)
+// The batched handle `handle` (pv_process etc.) is created with the same window.
+//
+// What differs by construction: no cuFFT plans (`plan`, `ifft` are 0), the
+// managed-memory attach calls do not exist, and STANDARD mode (an extension: the
+// textbook vocoder the reference never implemented) runs on `handle` directly.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
+#include "kernel.h"
 #include "pv.h"
 
 #ifndef PV_DEFAULT_MAX_FRAMES
 #define PV_DEFAULT_MAX_FRAMES 65536
 #endif
+#define NUM_STREAMS 3  // phaseVocoder.h:4
 
 enum Effect { TIME_SHIFT = 't', PITCH_SHIFT = 'p' };  // phaseVocoder.h:5-8
 
 class PhaseVocoder {
    public:
-    float* imp = nullptr;  // analysis/synthesis window (device), phaseVocoder.h:16
-    int hopSize = 0;       // phaseVocoder.h:25
-    int nSamps = 0;        // phaseVocoder.h:26
+    float* imp = nullptr;              // analysis/synthesis window (managed), phaseVocoder.h:16
+    float* imp1 = nullptr;             // phaseVocoder.h:17 (second window, unused by the path)
+    float* curr_input = nullptr;       // real-time buffers, phaseVocoder.h:18-22 (managed,
+    float* prev_input = nullptr;       //   allocated by the 1-argument constructor as in the
+    float* prev_output = nullptr;      //   reference; main.cpp:49 memcpys into curr_input)
+    float2* prev_mag_phase = nullptr;
+    float2* curr_mag_phase = nullptr;
+    int plan = 0, ifft = 0;  // the cuFFT plans have no counterpart (kept for source compat)
+    int hopSize = 0;         // phaseVocoder.h:25
+    int nSamps = 0;          // phaseVocoder.h:26
     int R = 1;
     int N = 0;
     float timeScale = 1.0f;  // phaseVocoder.h:29
     int outHopSize = 0;      // phaseVocoder.h:30
-    int plan = 0;            // the cuFFT plan handle has no counterpart (kept for source compat)
-    pv_handle* handle = nullptr;
+    int stream = 0;          // phaseVocoder.h:31
+    hipStream_t streams[NUM_STREAMS] = {};
+    pv_handle* handle = nullptr;  // batched C-ABI handle (same configuration and window)
 
     static void checkCUDAErrori(pv_status st, const char* msg, int line) {
         if (st != PV_OK) {  // phaseVocoder.h:35-44 / io.cpp:115-124: print + exit
@@ -44,14 +66,136 @@ class PhaseVocoder {
         }
     }
 
-    // phaseVocoder.h:46: PhaseVocoder(int samples) -> hop = samples/2, timeScale 1
-    explicit PhaseVocoder(int samples, pv_mode mode = PV_MODE_REF_COMPAT)
-        : PhaseVocoder(samples, TIME_SHIFT, 1.0f, 2, mode) {}
+    // phaseVocoder.h:46-78: hop = samples/2, timeScale 1, periodic Hann
+    // imp[i] = 0.5f*(1.f - cosf(2.f*M_PI*i/samples)); the real-time buffers are allocated
+    explicit PhaseVocoder(int samples, int max_frames = PV_DEFAULT_MAX_FRAMES, int device = 0) {
+        init(samples, TIME_SHIFT, 1.0f, 2, PV_MODE_REF_COMPAT, PV_WINDOW_HANN_REF, 1, max_frames, device);
+        std::vector<float> w(2 * (size_t)samples);  // imp1: 2N entries (the reference writes
+        for (int i = 0; i < 2 * samples; ++i)          // 2N into an N-float buffer)
+            w[i] = 0.5f * (1.f - cosf((float)(2.0 * M_PI * (double)i / (double)samples)));
+        imp1 = managed_copy(w.data(), 2 * (size_t)samples, "Malloc imp1 error");
+        prev_mag_phase = (float2*)managed_zero(sizeof(float) * 2 * samples, "Malloc prev_mag_phase error");
+        prev_input = (float*)managed_zero(sizeof(float) * samples, "Malloc prev_input");
+        prev_output = (float*)managed_zero(sizeof(float) * samples, "Malloc prev_output");
+        curr_mag_phase = (float2*)managed_zero(sizeof(float) * samples, "Malloc curr_mag_phase");
+        curr_input = (float*)managed_zero(sizeof(float) * samples, "Malloc curr_input");
+    }
 
-    // phaseVocoder.h:79-116: hop = samples / hop (the 4th argument is a divisor)
+    // phaseVocoder.h:79-116: hop = samples / hop (the 4th argument is a divisor), symmetric
+    // Hamming; TIME_SHIFT: outHopSize = scaleFactor*hopSize.  `mode` selects REF_COMPAT
+    // (the reference's path, default) or STANDARD (the textbook vocoder, an extension).
     PhaseVocoder(int samples, Effect e, float scaleFactor, int hop,
                  pv_mode mode = PV_MODE_REF_COMPAT, int max_channels = 1,
                  int max_frames = PV_DEFAULT_MAX_FRAMES, int device = 0) {
+        init(samples, e, scaleFactor, hop, mode, PV_WINDOW_DEFAULT, max_channels, max_frames, device);
+        const float omega1 = (float)(2.0 * M_PI / (2 * samples - 1));  // phaseVocoder.h:90-94
+        std::vector<float> w(samples);
+        for (int i = 0; i < samples; ++i) w[i] = 0.54f - 0.46f * cosf(omega1 * (float)i);
+        imp1 = managed_copy(w.data(), samples, "Malloc imp1 error");
+    }
+
+    PhaseVocoder(const PhaseVocoder&) = delete;
+    PhaseVocoder& operator=(const PhaseVocoder&) = delete;
+    ~PhaseVocoder() {  // phaseVocoder.h:128-130 frees imp; the rest is released here too
+        void* bufs[] = {imp, imp1, curr_input, prev_input, prev_output, prev_mag_phase, curr_mag_phase};
+        for (void* b : bufs)
+            if (b) (void)hipFree(b);
+        for (auto& s : streams)
+            if (s) (void)hipStreamDestroy(s);
+        pv_destroy(handle);
+    }
+
+    int specStride() const { return spec_stride_; }
+    pv_mode mode() const { return mode_; }
+
+    // phaseVocoder.h:118-126
+    hipStream_t* getStream() {
+        hipStream_t* out = &streams[stream++];
+        stream %= NUM_STREAMS;
+        return out;
+    }
+    hipStream_t* getPrevStream() { return &streams[(stream + NUM_STREAMS - 1) % NUM_STREAMS]; }
+
+    // phaseVocoder.cpp:25-33 -> kernel.cu:299-348: one nSamps frame -> `output`
+    // (2N float2 {mag, phase} in REF_COMPAT; N/2+1 in STANDARD)
+    void analysis_CUFFT(float* input, float2* output, float2* fft, float* intermediary) {
+        sync();
+        if (mode_ == PV_MODE_REF_COMPAT) {
+            CudaPhase::pv_analysis_CUFFT(output, fft, input, intermediary, imp, nSamps);
+        } else {
+            checkCUDAErrori(pv_analysis(handle, input, nSamps, nSamps, 1, 1, (pv_float2*)output,
+                                        spec_stride_, nullptr),
+                            "pv_analysis ", __LINE__);
+        }
+        sync();
+    }
+    // phaseVocoder.cpp:34-42 (hand-FFT path) -> CudaPhase::pv_analysis: same contract here
+    void analysis(float* input, float2* output, float2* fft, float* intermediary) {
+        analysis_CUFFT(input, output, fft, intermediary);
+    }
+
+    // phaseVocoder.cpp:60-76 -> kernel.cu:352-432: output[0..N) = frame(frontFrame) +
+    // backFrame[outHop..N) (cudaOverlapAdd, kernel.cu:111-119)
+    void resynthesis_CUFFT(float* backFrame, float2* frontFrame, float* output) {
+        sync();
+        if (mode_ == PV_MODE_REF_COMPAT) {
+            CudaPhase::resynthesis_CUFFT(output, backFrame, frontFrame, imp, nSamps, outHopSize);
+        } else {
+            checkCUDAErrori(pv_resynthesis(handle, (const pv_float2*)frontFrame, spec_stride_, 1, 1,
+                                           backFrame + outHopSize, nSamps, output, nSamps, nullptr),
+                            "resynthesis", __LINE__);
+        }
+        sync();
+    }
+    // phaseVocoder.cpp:44-58 (hand-FFT path) -> CudaPhase::resynthesis: same contract here
+    void resynthesis(float* backFrame, float2* frontFrame, float2* intermediary, float* output) {
+        if (mode_ == PV_MODE_REF_COMPAT) {
+            sync();
+            CudaPhase::resynthesis(output, backFrame, frontFrame, intermediary, imp, nSamps, outHopSize);
+            sync();
+        } else {
+            resynthesis_CUFFT(backFrame, frontFrame, output);
+        }
+    }
+    // phaseVocoder.cpp:77-78 declares the processing hook and leaves its body empty (the
+    // reference's planned processing stage, README.md:22-23).  Here the hook runs on the
+    // analysed spectrum `magFreq`, then the frame is resynthesised like resynthesis_CUFFT.
+    void resynthesis(float* backFrame, float2* magFreq, float* output, void (*processing)()) {
+        if (processing) processing();
+        resynthesis_CUFFT(backFrame, magFreq, output);
+    }
+
+    // phaseVocoder.cpp:20-23 -> kernel.cu:289-298: window, shift, unshift, window, OLA
+    // (identity processing: output = w^2 * input + backFrame tail)
+    void test_overlap_add(float* input, float* output, float* intermediary, float* backFrame, int n) {
+        sync();
+        CudaPhase::test_overlap_add(input, output, intermediary, backFrame, imp, n, hopSize);
+        sync();
+    }
+
+   private:
+    int spec_stride_ = 0;
+    pv_mode mode_ = PV_MODE_REF_COMPAT;
+
+    static void sync() {
+        if (hipStreamSynchronize(nullptr) != hipSuccess)
+            checkCUDAErrori(PV_ERR_HIP, "stream sync error", __LINE__);
+    }
+    static float* managed_copy(const float* src, size_t n, const char* what) {
+        float* p = nullptr;
+        if (hipMallocManaged((void**)&p, sizeof(float) * n) != hipSuccess) checkCUDAErrori(PV_ERR_HIP, what, __LINE__);
+        for (size_t i = 0; i < n; ++i) p[i] = src[i];
+        return p;
+    }
+    static void* managed_zero(size_t bytes, const char* what) {
+        void* p = nullptr;
+        if (hipMallocManaged(&p, bytes) != hipSuccess) checkCUDAErrori(PV_ERR_HIP, what, __LINE__);
+        std::memset(p, 0, bytes);
+        return p;
+    }
+
+    void init(int samples, Effect e, float scaleFactor, int hop, pv_mode mode, int window,
+              int max_channels, int max_frames, int device) {
         pv_config cfg{};
         cfg.n_samps = samples;
         cfg.hop_div = hop;
@@ -61,6 +205,8 @@ class PhaseVocoder {
         cfg.max_channels = max_channels;
         cfg.max_frames = max_frames;
         cfg.device = device;
+        cfg.window = window;
+        cfg.nan_faithful = CudaPhase::detail::nan_faithful_flag();
         checkCUDAErrori(pv_create(&cfg, &handle), "PhaseVocoder constructor", __LINE__);
         pv_info info{};
         pv_get_info(handle, &info);
@@ -69,73 +215,21 @@ class PhaseVocoder {
         outHopSize = info.out_hop;
         timeScale = (e == TIME_SHIFT) ? scaleFactor : 1.0f;
         spec_stride_ = info.spec_stride;
-        // imp: same recipe as phaseVocoder.h:85-89 (float omega, float cos)
+        mode_ = mode;
+        // imp: the constructor's recipe (float argument, float cos as in the reference)
         std::vector<float> w(samples);
-        const float omega = (float)(2.0 * 3.14159265358979323846 / (samples - 1));
-        for (int i = 0; i < samples; ++i) w[i] = 0.54f - 0.46f * cosf(omega * (float)i);
-        if (mode == PV_MODE_STANDARD)
+        if (mode == PV_MODE_STANDARD) {
             for (int i = 0; i < samples; ++i)
-                w[i] = (float)(0.5 - 0.5 * std::cos(2.0 * 3.14159265358979323846 * i / samples));
-        if (hipMalloc((void**)&imp, sizeof(float) * samples) != hipSuccess ||
-            hipMemcpy(imp, w.data(), sizeof(float) * samples, hipMemcpyHostToDevice) != hipSuccess)
-            checkCUDAErrori(PV_ERR_HIP, "Malloc imp error", __LINE__);
-    }
-
-    PhaseVocoder(const PhaseVocoder&) = delete;
-    PhaseVocoder& operator=(const PhaseVocoder&) = delete;
-    ~PhaseVocoder() {  // phaseVocoder.h:128-130
-        if (imp) (void)hipFree(imp);
-        pv_destroy(handle);
-    }
-
-    int specStride() const { return spec_stride_; }
-
-    // phaseVocoder.cpp:25-33 -> kernel.cu:299-348: one nSamps frame -> `output`
-    // (2N float2 {mag, phase} in REF_COMPAT; N/2+1 in STANDARD).  `fft`, `intermediary`
-    // are unused, as the reference's cuFFT path leaves `fft` untouched.
-    void analysis_CUFFT(float* input, float2* output, float2* fft, float* intermediary) {
-        (void)fft;
-        (void)intermediary;
-        checkCUDAErrori(pv_analysis(handle, input, nSamps, nSamps, 1, 1, (pv_float2*)output,
-                                    spec_stride_, nullptr),
-                        "pv_analysis ", __LINE__);
-        sync();
-    }
-    // phaseVocoder.cpp:34-42 (hand-FFT path): same contract on this implementation
-    void analysis(float* input, float2* output, float2* fft, float* intermediary) {
-        analysis_CUFFT(input, output, fft, intermediary);
-    }
-
-    // phaseVocoder.cpp:60-76 -> kernel.cu:352-432: output[0..N) = frame(frontFrame) +
-    // backFrame[outHop..N) (cudaOverlapAdd, kernel.cu:111-119)
-    void resynthesis_CUFFT(float* backFrame, float2* frontFrame, float* output) {
-        checkCUDAErrori(pv_resynthesis(handle, (const pv_float2*)frontFrame, spec_stride_, 1, 1,
-                                       backFrame + outHopSize, nSamps, output, nSamps, nullptr),
-                        "resynthesis", __LINE__);
-        sync();
-    }
-    // phaseVocoder.cpp:44-58 (hand-FFT path): same contract on this implementation
-    void resynthesis(float* backFrame, float2* frontFrame, float2* intermediary, float* output) {
-        (void)intermediary;
-        resynthesis_CUFFT(backFrame, frontFrame, output);
-    }
-
-    // phaseVocoder.cpp:20-23 -> kernel.cu:289-298: window, shift, unshift, window, OLA
-    // (identity processing: output = w^2 * input + backFrame tail)
-    void test_overlap_add(float* input, float* output, float* intermediary, float* backFrame, int n);
-
-   private:
-    int spec_stride_ = 0;
-    static void sync() {
-        if (hipStreamSynchronize(nullptr) != hipSuccess)
-            checkCUDAErrori(PV_ERR_HIP, "stream sync error", __LINE__);
+                w[i] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * i / samples));
+        } else if (window == PV_WINDOW_HANN_REF) {  // phaseVocoder.h:64-66
+            for (int i = 0; i < samples; ++i)
+                w[i] = 0.5f * (1.f - cosf((float)(2.0 * M_PI * (double)i / (double)samples)));
+        } else {  // phaseVocoder.h:85-89
+            const float omega = (float)(2.0 * M_PI / (samples - 1));
+            for (int i = 0; i < samples; ++i) w[i] = 0.54f - 0.46f * cosf(omega * (float)i);
+        }
+        imp = managed_copy(w.data(), samples, "Malloc imp error");
+        for (auto& s : streams)  // phaseVocoder.h:112-114
+            if (hipStreamCreate(&s) != hipSuccess) checkCUDAErrori(PV_ERR_HIP, "stream create", __LINE__);
     }
 };
-
-inline void PhaseVocoder::test_overlap_add(float* input, float* output, float* intermediary,
-                                           float* backFrame, int n) {
-    (void)intermediary;
-    checkCUDAErrori(pv_test_overlap_add(input, imp, backFrame, output, n, hopSize, nullptr),
-                    "test_overlap_add", __LINE__);
-    sync();
-}

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PV_ABI_VERSION 1
+#define PV_ABI_VERSION 2  /* 2: pv_config.window / nan_faithful, pv_set_window */
 
 typedef struct pv_handle pv_handle;
 
@@ -69,6 +69,15 @@ typedef enum pv_mode {
     PV_MODE_STANDARD = 1    /* textbook phase vocoder (Hann, unwrap, true frequency)     */
 } pv_mode;
 
+typedef enum pv_window {
+    PV_WINDOW_DEFAULT = 0,     /* the mode's window: REF_COMPAT the symmetric Hamming of the
+                                  4-argument constructor, STANDARD the periodic Hann        */
+    PV_WINDOW_HAMMING_REF = 1, /* 0.54f - 0.46f*cosf(w*i), w = (float)(2pi/(N-1))
+                                  (src/phaseVocoder.h:85-89; REF_COMPAT)                    */
+    PV_WINDOW_HANN_REF = 2     /* 0.5f*(1.f - cosf((float)(2pi*i/N))) of the 1-argument
+                                  constructor (src/phaseVocoder.h:64-66; REF_COMPAT)        */
+} pv_window;
+
 typedef struct pv_config {
     int n_samps;      /* N, window length: power of 2 in [256, 2048] (both modes)       */
     int hop_div;      /* hop = N / hop_div (phaseVocoder.h:79 4th argument is a divisor)  */
@@ -78,6 +87,10 @@ typedef struct pv_config {
     int max_channels; /* workspace capacity                                             */
     int max_frames;   /* workspace capacity, frames per channel                          */
     int device;       /* HIP device ordinal                                             */
+    int window;       /* pv_window (0 = the mode's default); STANDARD accepts only 0      */
+    int nan_faithful; /* REF_COMPAT: a bin with Re = Im = 0 gets phase atanf(0/0) = NaN as
+                         in the reference (kernel.cu:101-109), which poisons that frame's
+                         resynthesis; 0 (default) gives phase 0 (SURVEY.md §8c deviation 4) */
 } pv_config;
 
 typedef struct pv_info {
@@ -171,6 +184,15 @@ pv_status pv_harmonize(pv_harmonizer* hz, const float* x, long long ldx, long lo
  * pointers on the current HIP device; the first call per (device, n) builds that size's
  * twiddle table (allocation: not capturable), later calls are. */
 pv_status pv_fft_c2c(const pv_float2* in, pv_float2* out, int n, int batch, int inverse, void* stream);
+
+/* REF_COMPAT: replace the handle's window by the caller's (device pointer, n_samps
+ * floats; copied on `stream`, the pointer is not kept).  The reference passes the window
+ * to every call (CudaPhase::pv_analysis_CUFFT / resynthesis_CUFFT `win`, kernel.cu:301
+ * and :406): it multiplies the analysis frame and the resynthesised frame.  Here the
+ * analysis window becomes `win` and the synthesis gain win[k]/N (cudaDivVec kernel.cu:380
+ * then cudaWindow :406).  STANDARD handles: PV_ERR_UNSUPPORTED (their synthesis
+ * normalisation is derived from the Hann window at pv_create). */
+pv_status pv_set_window(pv_handle* h, const float* win, void* stream);
 
 /* Constant tables of a handle (windows, gains, twiddles, unwrap tables, pitch map) as one
  * device blob, so that one rank can build them and the others receive them over RCCL

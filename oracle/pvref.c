@@ -47,6 +47,14 @@ void pvr_hamming_ref(int N, float* w) {
     }
 }
 
+void pvr_hann_ref(int N, float* w) {
+    /* phaseVocoder.h:64-66, PhaseVocoder(int samples):
+     * imp[i] = 0.5f * (1.f - cosf(2.f*M_PI*i / samples));  -- 2.f*M_PI is double, so the
+     * argument is evaluated in double and converted to float for cosf. */
+    for (int i = 0; i < N; ++i)
+        w[i] = 0.5f * (1.f - cosf((float)(2.0 * PVR_PI_D * (double)i / (double)N)));
+}
+
 void pvr_fft_twiddles(int L, pvr_c32* tw) {
     for (int m = 0; m < L / 2; ++m) {
         double a = 2.0 * PVR_PI_D * (double)m / (double)L;
@@ -484,17 +492,23 @@ void pvr_compat_resynth_frame(const pvr_c64* spec, int N, const float* win, doub
 }
 
 int pvr_compat_process(const float* x, long n, int N, int hop_div, int frames, double* out) {
+    return pvr_compat_process_ex(x, n, N, hop_div, frames, NULL, 0, out);
+}
+
+int pvr_compat_process_ex(const float* x, long n, int N, int hop_div, int frames,
+                          const float* window, int nan_faithful, double* out) {
     const int hop = N / hop_div;
     float* win = (float*)malloc(sizeof(float) * N);
     float* frame = (float*)malloc(sizeof(float) * N);
     pvr_c64* spec = (pvr_c64*)malloc(sizeof(pvr_c64) * 2 * N);
     double* front = (double*)malloc(sizeof(double) * N);
     double* back = (double*)calloc(N, sizeof(double));
-    pvr_hamming_ref(N, win);
+    if (window) memcpy(win, window, sizeof(float) * N);  /* the caller's imp (kernel.cu:301, :406) */
+    else pvr_hamming_ref(N, win);
     for (int i = 0; i < frames; ++i) {
         long start = (long)i * hop;
         for (int k = 0; k < N; ++k) frame[k] = (start + k < n) ? x[start + k] : 0.0f;
-        pvr_compat_analysis_frame(frame, N, win, spec, 0);
+        pvr_compat_analysis_frame(frame, N, win, spec, nan_faithful);
         pvr_compat_resynth_frame(spec, N, win, front);
         /* cudaOverlapAdd (kernel.cu:111-119): front[k-hop] += back[k], k in [hop, N);
          * then main.cpp:279 backFrame <- final_output; emit backFrame[0..hop) */

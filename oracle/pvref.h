@@ -45,6 +45,7 @@ enum { PVR_TIME_SHIFT = 't', PVR_PITCH_SHIFT = 'p' };
 /* ---------------- tables (double -> float recipes) ---------------- */
 void pvr_hann_periodic(int N, float* w);                 /* 0.5-0.5cos(2 pi n/N)       */
 void pvr_hamming_ref(int N, float* w);                   /* phaseVocoder.h:85-89        */
+void pvr_hann_ref(int N, float* w);                      /* phaseVocoder.h:64-66 (1-arg)*/
 void pvr_fft_twiddles(int L, pvr_c32* tw);               /* L/2 entries e^{-2 pi i m/L} */
 void pvr_split_twiddles(int N, pvr_c32* tws);            /* N/2+1 entries e^{-2pi i k/N}*/
 void pvr_expected_advance(int N, int hop, float* e, int* j); /* N/2+1: e_k, j_k        */
@@ -80,6 +81,11 @@ void pvr_compat_resynth_frame(const pvr_c64* spec2N, int N, const float* win, do
 /* whole signal: analysis of `frames` frames, running OLA (main.cpp:253-297) over
  * `frames` resynthesis frames; out has frames*hop + N - hop samples. Returns hop. */
 int pvr_compat_process(const float* x, long n, int N, int hop_div, int frames, double* out);
+/* same with the caller's window (NULL = the 4-argument constructor's Hamming) and the
+ * NaN-faithful phase of all-zero bins (kernel.cu:101-109; NaN then poisons the frame's
+ * resynthesis and the N samples of overlap-add it touches, as in the reference). */
+int pvr_compat_process_ex(const float* x, long n, int N, int hop_div, int frames,
+                          const float* window, int nan_faithful, double* out);
 
 /* ---------------- fp64 helpers (exposed for tests) ---------------- */
 void pvr_fft_c64(pvr_c64* data, int L, int inverse);     /* unnormalised radix-2 DIT    */

@@ -37,6 +37,7 @@ def lib():
         c_long, c_int, c_float = ctypes.c_long, ctypes.c_int, ctypes.c_float
         L.pvr_hann_periodic.argtypes = [c_int, _f32p]
         L.pvr_hamming_ref.argtypes = [c_int, _f32p]
+        L.pvr_hann_ref.argtypes = [c_int, _f32p]
         L.pvr_fft_twiddles.argtypes = [c_int, _f32p]
         L.pvr_split_twiddles.argtypes = [c_int, _f32p]
         L.pvr_expected_advance.argtypes = [c_int, c_int, _f32p, _i32p]
@@ -57,6 +58,8 @@ def lib():
         L.pvr_compat_resynth_frame.argtypes = [_f64p, c_int, _f32p, _f64p]
         L.pvr_compat_process.argtypes = [_f32p, c_long, c_int, c_int, c_int, _f64p]
         L.pvr_compat_process.restype = c_int
+        L.pvr_compat_process_ex.argtypes = [_f32p, c_long, c_int, c_int, c_int, ctypes.c_void_p, c_int, _f64p]
+        L.pvr_compat_process_ex.restype = c_int
         L.pvr_fft_c64.argtypes = [_f64p, c_int, c_int]
         L.pvr_std_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                             c_float, c_int, _f32p, c_long, c_int]
@@ -73,6 +76,13 @@ def _c32(a):
 def hann_periodic(N):
     w = np.empty(N, np.float32)
     lib().pvr_hann_periodic(N, w)
+    return w
+
+
+def hann_ref(N):
+    """PhaseVocoder(int samples) window (phaseVocoder.h:64-66)."""
+    w = np.empty(N, np.float32)
+    lib().pvr_hann_ref(N, w)
     return w
 
 
@@ -187,11 +197,15 @@ def compat_analysis_frame(frame, N, nan_faithful=False):
     return b.view(np.complex128)  # (mag + i*phase) per bin, 2N bins
 
 
-def compat_process(x, N, hop_div, frames=None):
+def compat_process(x, N, hop_div, frames=None, window=None, nan_faithful=False):
+    """REF_COMPAT whole-signal path; window: float32[N] (None = the Hamming of the
+    4-argument constructor)."""
     x = _c32(x)
     hop = N // hop_div
     if frames is None:
         frames = num_frames(x.shape[0], hop)
     out = np.zeros(frames * hop + (N - hop), np.float64)
-    lib().pvr_compat_process(x, x.shape[0], N, hop_div, frames, out)
+    w = None if window is None else _c32(window)
+    lib().pvr_compat_process_ex(x, x.shape[0], N, hop_div, frames,
+                                None if w is None else w.ctypes.data, 1 if nan_faithful else 0, out)
     return out

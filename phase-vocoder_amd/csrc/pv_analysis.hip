@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     };
     // frames whose N samples are all inside [0, n) take the vector-load path; the (at most
     // N/hop) frames at the end of a channel take the bounds-checked path.
-    const long long lastfull = p.aligned ? (p.n - N) / p.hop : -1;  // last frame fully inside
+    // last frame fully inside: floor((n - N) / hop), -1 when n < N (C++ division truncates
+    // toward zero, which for N - hop < n < N would give 0 and read frame 0 past the end)
+    const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
     if (t0 > 0) {
         float2 xh[E], z[E];
         if (t0 - 1 <= lastfull) load_fast(-1, xh); else load_checked(-1, xh);

@@ -52,6 +52,13 @@ void hann_periodic(int N, std::vector<float>& w) {
         w[n] = (float)(0.5 - 0.5 * std::cos(2.0 * kPi * (double)n / (double)N));
 }
 
+void hann_ref(int N, std::vector<float>& w) {
+    // phaseVocoder.h:64-66 (1-argument constructor): 0.5f * (1.f - cosf(2.f*M_PI*i / samples));
+    // 2.f*M_PI*i/samples is evaluated in double and rounded to float for cosf
+    w.resize(N);
+    for (int i = 0; i < N; ++i) w[i] = 0.5f * (1.f - cosf((float)(2.0 * kPi * (double)i / (double)N)));
+}
+
 void hamming_ref(int N, std::vector<float>& w) {
     // phaseVocoder.h:85-89
     w.resize(N);
@@ -93,7 +100,7 @@ struct pv_handle {
     pv_config cfg{};
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
-    int mode = 0, effect = 0, pitch = 0, aligned_hop = 1;
+    int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
     int q_pow2 = 1;
@@ -194,7 +201,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.spec_stride = h->spec_stride;
     p.runsum = want_runsum ? h->d_runsum : nullptr;
     p.bins_pad = h->bins_pad;
-    p.nan_faithful = 0;
+    p.nan_faithful = h->nan_faithful;
     if (h->mode == PV_MODE_STANDARD)
         PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
     else
@@ -363,6 +370,10 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: n_samps in [256, 2048]");
     if (cfg->mode == PV_MODE_REF_COMPAT && (N < 256 || N > 2048))
         return fail(PV_ERR_UNSUPPORTED, "REF_COMPAT mode: n_samps in [256, 2048]");
+    if (cfg->window < PV_WINDOW_DEFAULT || cfg->window > PV_WINDOW_HANN_REF)
+        return fail(PV_ERR_ARG, "unknown window");
+    if (cfg->mode == PV_MODE_STANDARD && cfg->window != PV_WINDOW_DEFAULT)
+        return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: the periodic Hann window only (window = 0)");
 
     pv_handle* h = new pv_handle();
     h->cfg = *cfg;
@@ -370,6 +381,7 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     h->mode = cfg->mode;
     h->effect = cfg->effect;
     h->scale = cfg->scale;
+    h->nan_faithful = (cfg->mode == PV_MODE_REF_COMPAT && cfg->nan_faithful) ? 1 : 0;
     h->hop = N / cfg->hop_div;  // phaseVocoder.h:79
     if (cfg->effect == PV_TIME_SHIFT) {
         float f = cfg->scale * (float)h->hop;  // phaseVocoder.h:104 (float -> int)
@@ -434,7 +446,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         }
         for (int i = 0; i < N; ++i) gain[i] = (float)(wd[i] * ((double)h->hs / sw2) / (double)N);
     } else {
-        hamming_ref(N, win);
+        if (cfg->window == PV_WINDOW_HANN_REF) hann_ref(N, win);  // PhaseVocoder(int samples)
+        else hamming_ref(N, win);
         for (int i = 0; i < N; ++i) gain[i] = win[i] / (float)N;  // kernel.cu:380 /N, :406 window
     }
     if ((st = upload(&h->d_win, win)) != PV_OK) return bail(st);
@@ -647,6 +660,16 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
         off += align16(sg.bytes);
     }
     PV_HIP(hipStreamSynchronize(s));
+    return PV_OK;
+}
+
+pv_status pv_set_window(pv_handle* h, const float* win, void* stream) {
+    if (!h || !win) return fail(PV_ERR_ARG, "null argument");
+    if (h->mode != PV_MODE_REF_COMPAT)
+        return fail(PV_ERR_UNSUPPORTED, "pv_set_window: REF_COMPAT handles only");
+    DeviceGuard g(h->cfg.device);
+    hipError_t e = pv::launch_window_gain(win, h->d_win, h->d_gain, h->N, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("pv_set_window: ") + hipGetErrorString(e));
     return PV_OK;
 }
 

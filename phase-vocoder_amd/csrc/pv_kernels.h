@@ -119,6 +119,7 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
 hipError_t launch_mix(const MixParams& p, hipStream_t s);
 hipError_t launch_rt(int L, int mode, const RtParams& p, hipStream_t s);
 size_t rt_lds_bytes(int L);
+hipError_t launch_window_gain(const float* win, float* dwin, float* gain, int n, hipStream_t s);
 hipError_t launch_overlap_test(const float* in, const float* win, const float* back, float* out,
                                int n, int hop, hipStream_t s);
 

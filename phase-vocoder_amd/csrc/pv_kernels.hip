@@ -467,6 +467,23 @@ hipError_t launch_overlap_test(const float* in, const float* win, const float* b
     return hipGetLastError();
 }
 
+// pv_set_window (REF_COMPAT): the caller's window becomes the analysis window and the
+// synthesis gain win/N (kernel.cu:380 cudaDivVec then :406 cudaWindow; N is a power of two,
+// so win * (1/N) is exactly win / N).
+__global__ __launch_bounds__(256) void k_window_gain(const float* __restrict__ win, float* __restrict__ dwin,
+                                                     float* __restrict__ gain, int n, float inv_n) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const float w = win[k];
+    dwin[k] = w;
+    gain[k] = w * inv_n;
+}
+
+hipError_t launch_window_gain(const float* win, float* dwin, float* gain, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_window_gain, dim3((n + 255) / 256), dim3(256), 0, s, win, dwin, gain, n, 1.0f / (float)n);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers
 template <int L>
 static size_t syn_lds(int dt) {

@@ -9,8 +9,13 @@
 //     --N 256 --hopdiv 2 --scale 1       PhaseVocoder(256, effect, 1, 2)  (main.cpp:84)
 //     --mode ref|std                     REF_COMPAT (default) or PV_STANDARD
 //     --batched                          all channels in one pv_process call
+//     --single-arg                       PhaseVocoder(N): periodic Hann, hop N/2 (phaseVocoder.h:46-78)
+//     --nan-faithful                     atanf(0/0) = NaN phases as the reference (kernel.cu:101-109)
+//     --timer                            print CudaPhase::timer() per call (main.cpp:238-241, 275-278)
 //     --dump-f32 <file>                  raw float32 of the emitted channel-0 samples
 //
+// The per-frame REF_COMPAT calls go PhaseVocoder -> CudaPhase (include/kernel.h) with the
+// object's window, as phaseVocoder.cpp -> kernel.cu do.
 // Per-frame mode reproduces main.cpp:204-309: analysis_CUFFT of every channel's frames
 // i = 0, hop, ... < n - hop into pre-zeroed 2N-bin spectra; resynthesis of frames
 // i < n/outHop with the running backFrame (main.cpp:253-297); only channel 0 is
@@ -21,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,7 +48,8 @@ int main(int argc, char** argv) {
     Effect effect = TIME_SHIFT;
     int N = 256, hopdiv = 2;
     float scale = 1.0f;
-    bool batched = false;
+    bool batched = false, single_arg = false, show_timer = false;
+    double ana_ms = 0.0, syn_ms = 0.0;
     pv_mode mode = PV_MODE_REF_COMPAT;
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
@@ -52,6 +59,9 @@ int main(int argc, char** argv) {
         else if (a == "--scale" && i + 1 < argc) scale = (float)std::atof(argv[++i]);
         else if (a == "--mode" && i + 1 < argc) mode = std::string(argv[++i]) == "std" ? PV_MODE_STANDARD : PV_MODE_REF_COMPAT;
         else if (a == "--batched") batched = true;
+        else if (a == "--single-arg") single_arg = true;
+        else if (a == "--nan-faithful") CudaPhase::set_nan_faithful(true);
+        else if (a == "--timer") show_timer = true;
         else if (a == "--dump-f32" && i + 1 < argc) dump = argv[++i];
         else pos.push_back(a);
     }
@@ -71,11 +81,19 @@ int main(int argc, char** argv) {
     std::printf("channels %d, samples per channel %d, rate %d, bits %d\n", numChannels, numSamples,
                 audio.sample_rate, audio.bit_depth);
 
+    if (single_arg) {  // PhaseVocoder(int samples): hop N/2, timeScale 1, REF_COMPAT
+        hopdiv = 2;
+        scale = 1.0f;
+        mode = PV_MODE_REF_COMPAT;
+    }
     const int hop = N / hopdiv;
     const int frames = pv_frame_count(numSamples, hop);
     const int padN = numSamples + 2 * N;  // frames near the end read zeros (deviation 1)
-    PhaseVocoder phase(N, effect, scale, hopdiv, mode, numChannels > 0 ? numChannels : 1,
-                       frames + numSamples / std::max(1, (int)(scale * hop)) + 2);
+    const int cap = frames + numSamples / std::max(1, (int)(scale * hop)) + 2;
+    std::unique_ptr<PhaseVocoder> owner(
+        single_arg ? new PhaseVocoder(N, cap)                                     // main.cpp:84 analogue
+                   : new PhaseVocoder(N, effect, scale, hopdiv, mode, numChannels > 0 ? numChannels : 1, cap));
+    PhaseVocoder& phase = *owner;
     const int outLen = (int)(phase.timeScale * numSamples);
     std::vector<std::vector<float>> outFile(2, std::vector<float>(outLen > 0 ? outLen : 0, 0.f));
 
@@ -117,8 +135,11 @@ int main(int argc, char** argv) {
         std::printf("analysis...\n");
         for (int channel = 0; channel < numChannels; channel++)                  // main.cpp:228
             for (int i = 0; i < numSamples - hop; i += hop)                       // main.cpp:231
+            {
                 phase.analysis_CUFFT(d_input + (size_t)channel * padN + i,
                                      d_output + ((size_t)channel * nspec + i / hop) * S, nullptr, nullptr);
+                ana_ms += CudaPhase::timer().getGpuElapsedTimeForPreviousOperation();  // main.cpp:240
+            }
         float *backFrame = nullptr, *final_output = nullptr;
         HIPCHECK(hipMalloc((void**)&backFrame, sizeof(float) * N));
         HIPCHECK(hipMalloc((void**)&final_output, sizeof(float) * N));
@@ -131,6 +152,7 @@ int main(int argc, char** argv) {
             for (int i = 0; i < numSamples / phase.outHopSize; i++) {            // main.cpp:266
                 const int si = i < nspec ? i : nspec - 1;
                 phase.resynthesis_CUFFT(backFrame, d_output + ((size_t)channel * nspec + si) * S, final_output);
+                syn_ms += CudaPhase::timer().getGpuElapsedTimeForPreviousOperation();  // main.cpp:277
                 HIPCHECK(hipMemcpy(backFrame, final_output, sizeof(float) * N, hipMemcpyDeviceToDevice));
                 HIPCHECK(hipMemcpy(h.data(), backFrame, sizeof(float) * N, hipMemcpyDeviceToHost));
                 for (int j = 0; j < phase.outHopSize; j++) {
@@ -149,6 +171,8 @@ int main(int argc, char** argv) {
         HIPCHECK(hipFree(d_output));
     }
     HIPCHECK(hipFree(d_input));
+    if (show_timer && !batched)
+        std::printf("CudaPhase::timer(): analysis %.3f ms total, resynthesis %.3f ms total\n", ana_ms, syn_ms);
     std::printf("writing to file\n");
     if (!pvwav::save16(out, outFile, 44100)) {
         std::printf("err: could not write %s\n", out.c_str());

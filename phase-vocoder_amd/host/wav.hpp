@@ -95,7 +95,9 @@ inline bool save16(const std::string& path, const std::vector<std::vector<float>
         for (int c = 0; c < ch; ++c) {
             float v = s[c][i];
             v = v > 1.f ? 1.f : (v < -1.f ? -1.f : v);
-            const int16_t q = (int16_t)(v * 32767.);  // AudioFile.h:1045-1049
+            // AudioFile.h:1045-1049; NaN (REF_COMPAT nan_faithful) -> 0, what the reference's
+            // undefined (int16_t)(NaN) gives on x86 (cvttsd2si 0x80000000, low 16 bits)
+            const int16_t q = (v != v) ? (int16_t)0 : (int16_t)(v * 32767.);
             put(&q, 2);
         }
     std::ofstream f(path, std::ios::binary);

@@ -14,6 +14,7 @@ HEADER = os.path.join(ROOT, "include", "pv.h")
 PV_OK, PV_ERR_ARG, PV_ERR_UNSUPPORTED, PV_ERR_HIP, PV_ERR_NOMEM = range(5)
 PV_TIME_SHIFT, PV_PITCH_SHIFT = ord("t"), ord("p")
 PV_MODE_REF_COMPAT, PV_MODE_STANDARD = 0, 1
+PV_WINDOW_DEFAULT, PV_WINDOW_HAMMING_REF, PV_WINDOW_HANN_REF = 0, 1, 2
 
 
 class PVError(RuntimeError):
@@ -25,7 +26,8 @@ class PVError(RuntimeError):
 class pv_config(ctypes.Structure):
     _fields_ = [("n_samps", ctypes.c_int), ("hop_div", ctypes.c_int), ("effect", ctypes.c_int),
                 ("scale", ctypes.c_float), ("mode", ctypes.c_int), ("max_channels", ctypes.c_int),
-                ("max_frames", ctypes.c_int), ("device", ctypes.c_int)]
+                ("max_frames", ctypes.c_int), ("device", ctypes.c_int), ("window", ctypes.c_int),
+                ("nan_faithful", ctypes.c_int)]
 
 
 class pv_info(ctypes.Structure):
@@ -77,6 +79,8 @@ def lib():
     L.pv_export_tables.restype = i
     L.pv_import_tables.argtypes = [vp, vp, ctypes.c_size_t, vp]
     L.pv_import_tables.restype = i
+    L.pv_set_window.argtypes = [vp, vp, vp]
+    L.pv_set_window.restype = i
     L.pv_test_overlap_add.argtypes = [vp, vp, vp, vp, i, i, vp]
     L.pv_test_overlap_add.restype = i
     L.pv_profile_enable.argtypes = [vp, i]

@@ -41,12 +41,18 @@ class PhaseVocoder:
 
     def __init__(self, samples: int, effect: str = TIME_SHIFT, scaleFactor: float = 1.0,
                  hop: int = 2, *, mode: str = REF_COMPAT, max_channels: int = 1,
-                 max_frames: int = 4096, device: int = 0, exit_on_error: bool = False):
+                 max_frames: int = 4096, device: int = 0, exit_on_error: bool = False,
+                 window: int = _lib.PV_WINDOW_DEFAULT, nan_faithful: bool = False):
+        """window: PV_WINDOW_DEFAULT (the mode's), PV_WINDOW_HAMMING_REF or
+        PV_WINDOW_HANN_REF (the 1-argument constructor's, phaseVocoder.h:64-66; see
+        `single_arg`); nan_faithful: REF_COMPAT atanf(0/0) = NaN (kernel.cu:101-109)."""
         self.exit_on_error = exit_on_error
         eff = effect if isinstance(effect, int) else ord(effect)
         m = PV_MODE_REF_COMPAT if mode == REF_COMPAT else PV_MODE_STANDARD
         cfg = _lib.pv_config(int(samples), int(hop), eff, float(scaleFactor), m,
-                             int(max_channels), int(max_frames), int(device))
+                             int(max_channels), int(max_frames), int(device), int(window),
+                             1 if nan_faithful else 0)
+        self.window = int(window)
         h = ctypes.c_void_p()
         self._L = _lib.lib()
         self._call(self._L.pv_create(ctypes.byref(cfg), ctypes.byref(h)), "pv_create")
@@ -66,6 +72,19 @@ class PhaseVocoder:
         self.spec_bins = info.spec_bins
         self.spec_stride = info.spec_stride
         self.frames_per_run = info.frames_per_run
+
+    @classmethod
+    def single_arg(cls, samples: int, **kw):
+        """`PhaseVocoder(int samples)` (src/phaseVocoder.h:46-78): hop = samples/2,
+        timeScale 1, periodic Hann window 0.5f*(1 - cosf(2 pi i/N))."""
+        return cls(samples, TIME_SHIFT, 1.0, 2, mode=REF_COMPAT,
+                   window=_lib.PV_WINDOW_HANN_REF, **kw)
+
+    def set_window(self, win, stream=None):
+        """REF_COMPAT: use the caller's window (CUDA float32 tensor of nSamps) for the
+        analysis and the resynthesis, as CudaPhase::*_CUFFT's `win` (kernel.cu:301, :406)."""
+        assert win.is_cuda and win.numel() == self.nSamps and win.is_contiguous()
+        self._call(self._L.pv_set_window(self._h, _ptr(win), self._stream(stream)), "pv_set_window")
 
     # -------------------------------------------------------------- plumbing
     def _call(self, status, what):
@@ -103,7 +122,7 @@ class PhaseVocoder:
     def imp(self) -> np.ndarray:
         """Analysis window (phaseVocoder.h:16 `imp`), host copy."""
         from .tables import analysis_window
-        return analysis_window(self.nSamps, self.mode)
+        return analysis_window(self.nSamps, self.mode, self.window)
 
     # -------------------------------------------------------------- geometry
     def num_frames(self, n_samples: int) -> int:

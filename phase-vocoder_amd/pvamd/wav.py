@@ -78,7 +78,9 @@ def encode16(samples: np.ndarray, sample_rate: int = 44100) -> bytes:
     """samples [channels, n] -> 16-bit PCM WAV bytes (AudioFile::saveToWaveFile)."""
     s = np.atleast_2d(np.asarray(samples, dtype=np.float64))
     ch, n = s.shape
-    ints = np.trunc(np.clip(s, -1.0, 1.0) * 32767.0).astype("<i2")
+    # NaN (REF_COMPAT nan_faithful output) -> 0: the reference's undefined int16 cast of NaN
+    # gives 0 on x86 (cvttsd2si -> 0x80000000, low 16 bits)
+    ints = np.trunc(np.nan_to_num(np.clip(s, -1.0, 1.0), nan=0.0) * 32767.0).astype("<i2")
     body = ints.T.reshape(-1).tobytes()
     hdr = b"RIFF" + struct.pack("<i", 4 + 24 + 8 + len(body)) + b"WAVE"
     hdr += b"fmt " + struct.pack("<ihhiihh", 16, 1, ch, sample_rate, ch * sample_rate * 2, ch * 2, 16)

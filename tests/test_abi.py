@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.pv_abi_version() == 1
+    assert L.pv_abi_version() == 2
     assert L.pv_status_string(0) == b"PV_OK"
     assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
 
@@ -55,7 +55,9 @@ def test_create_rejects_bad_configs_without_touching_gpu():
                 _lib.pv_config(1024, 0, ord("t"), 1.0, 1, 1, 10, 0),   # hop_div 0
                 _lib.pv_config(1024, 4, ord("x"), 1.0, 1, 1, 10, 0),   # bad effect
                 _lib.pv_config(1024, 4, ord("t"), -1.0, 1, 1, 10, 0),  # bad scale
-                _lib.pv_config(1024, 4, ord("p"), 2.0, 0, 1, 10, 0)):  # compat has no pitch
+                _lib.pv_config(1024, 4, ord("p"), 2.0, 0, 1, 10, 0),   # compat has no pitch
+                _lib.pv_config(1024, 4, ord("t"), 1.0, 0, 1, 10, 0, 7),  # unknown window
+                _lib.pv_config(1024, 4, ord("t"), 1.0, 1, 1, 10, 0, 2)):  # STANDARD: Hann only
         st = L.pv_create(ctypes.byref(cfg), ctypes.byref(h))
         assert st in (_lib.PV_ERR_ARG, _lib.PV_ERR_UNSUPPORTED)
         assert len(L.pv_last_error()) > 0

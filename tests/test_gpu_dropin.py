@@ -121,3 +121,113 @@ def test_overlap_test_identity(cuda):
     ref = (x * w) * w
     ref[:N - hop] += b[hop:]
     assert np.allclose(out.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
+
+
+# ------------------------------------------------------------ config 1 at full size
+REF_440 = os.path.join(GOLDEN, "testtones_440sine.wav")  # the reference's testtones/440sine.wav
+
+
+def run_main(args, timeout=300):
+    r = subprocess.run([PV_MAIN] + args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def check_wav_1lsb(out_wav, ref, n_total, n_emit):
+    s, sr, bits = wav.load(out_wav)
+    assert s.shape == (2, n_total) and bits == 16 and sr == 44100
+    assert np.array_equal(s[0], s[1])                      # R duplicates L (main.cpp:288-289)
+    q = np.trunc(np.nan_to_num(np.clip(ref[:n_emit], -1, 1)) * 32767) / 32768.0
+    assert np.max(np.abs(s[0, :n_emit] - q)) <= 1.01 / 32768  # within 1 LSB
+    assert np.all(s[0, n_emit:] == 0)                        # never written (main.cpp:266)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_config1_full_440sine_wav(cuda, tmp_path, batched):
+    """BASELINE configs[0] on the whole reference input: testtones/440sine.wav (441000
+    stereo frames, data chunk 2 bytes short), N=1024 hop 256, REF_COMPAT, scale 1: all
+    1722 frames of channel 0 through main.cpp's loop (per frame: PhaseVocoder ->
+    CudaPhase::*_CUFFT of include/kernel.h, timed by CudaPhase::timer()) vs the oracle."""
+    x = wav.load(REF_440)[0][0]
+    assert len(x) == 441000
+    out_wav, dump = str(tmp_path / "out.wav"), str(tmp_path / "out.f32")
+    args = [REF_440, "t", out_wav, "--N", "1024", "--hopdiv", "4", "--dump-f32", dump]
+    stdout = run_main(args + (["--batched"] if batched else ["--timer"]))
+    ref = pvref.compat_process(x, 1024, 4)
+    assert pvref.num_frames(len(x), 256) == 1722
+    n_emit = (len(x) // 256) * 256                             # 1722 resynthesis frames
+    got = np.fromfile(dump, np.float32)
+    assert len(got) >= n_emit
+    assert rms(got[:n_emit], ref[:n_emit]) <= 1e-5
+    frame_rms = np.sqrt(np.mean((got[:n_emit] - ref[:n_emit]).reshape(-1, 256) ** 2, axis=1))
+    assert frame_rms.max() <= 1e-5                             # every emitted hop, not only the mean
+    check_wav_1lsb(out_wav, ref, len(x), n_emit)
+    if not batched:
+        line = [ln for ln in stdout.splitlines() if ln.startswith("CudaPhase::timer()")][0]
+        assert float(line.split("analysis ")[1].split(" ms")[0]) > 0
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_single_arg_constructor_hann(cuda, tmp_path, batched):
+    """PhaseVocoder(int samples) (phaseVocoder.h:46-78): periodic Hann
+    0.5f*(1 - cosf(2 pi i/N)), hop N/2, timeScale 1.  Per frame the window reaches the
+    kernels only through CudaPhase's `win` argument (pv_set_window), so this also checks
+    that kernel.h honours the caller's window (kernel.cu:301, :406)."""
+    x = wav.load(REF_440)[0][0]
+    out_wav, dump = str(tmp_path / "o.wav"), str(tmp_path / "o.f32")
+    run_main([REF_440, "t", out_wav, "--N", "1024", "--single-arg", "--dump-f32", dump]
+             + (["--batched"] if batched else []))
+    ref = pvref.compat_process(x, 1024, 2, window=pvref.hann_ref(1024))
+    ham = pvref.compat_process(x, 1024, 2)
+    n_emit = (len(x) // 512) * 512
+    got = np.fromfile(dump, np.float32)[:n_emit]
+    assert rms(got, ref[:n_emit]) <= 1e-5
+    assert rms(got, ham[:n_emit]) > 1e-3                       # the window really differs
+    check_wav_1lsb(out_wav, ref, len(x), n_emit)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_nan_faithful_leading_silence(cuda, tmp_path, batched):
+    """kernel.cu:101-109: atanf(0/0) = NaN for the all-zero bins of digital silence (as at
+    the start of testtones/autotune.wav, 1124 zeros) poisons those frames' resynthesis and
+    the overlap-add samples they reach; the default (deviation 4) gives phase 0 instead."""
+    x = wav.load(REF_440)[0][0][:60000].copy()
+    x[:3000] = 0.0                                             # frames 0..7 entirely silent
+    path = str(tmp_path / "sil.wav")
+    write_pcm16(path, x)
+    dump, dump0 = str(tmp_path / "nan.f32"), str(tmp_path / "zero.f32")
+    common = [path, "t", str(tmp_path / "o.wav"), "--N", "1024", "--hopdiv", "4"] + (["--batched"] if batched else [])
+    run_main(common + ["--nan-faithful", "--dump-f32", dump])
+    run_main(common + ["--dump-f32", dump0])
+    n_emit = (len(x) // 256) * 256
+    got = np.fromfile(dump, np.float32)[:n_emit]
+    ref = pvref.compat_process(x, 1024, 4, nan_faithful=True)[:n_emit]
+    assert np.isnan(ref).sum() > 1000
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    assert rms(got[fin], ref[fin]) <= 1e-5
+    got0 = np.fromfile(dump0, np.float32)[:n_emit]
+    assert np.all(np.isfinite(got0))
+    assert rms(got0, pvref.compat_process(x, 1024, 4)[:n_emit]) <= 1e-5
+
+
+def test_python_mirror_single_arg_and_set_window(cuda):
+    import torch
+    from pvamd import _lib
+    x = np.load(os.path.join(GOLDEN, "sine440_ch0_32768.npy"))
+    pv = PhaseVocoder.single_arg(1024, max_frames=128)
+    assert (pv.hopSize, pv.outHopSize, pv.timeScale) == (512, 512, 1.0)
+    assert np.array_equal(pv.imp, pvref.hann_ref(1024))
+    out, _ = pv.process(torch.from_numpy(x).cuda())
+    assert rms(out.cpu().numpy()[0], pvref.compat_process(x, 1024, 2, window=pvref.hann_ref(1024))) <= 1e-5
+    # an arbitrary caller window (CudaPhase `win`) on a 4-argument handle
+    w = (0.3 + 0.7 * np.random.default_rng(3).random(1024)).astype(np.float32)
+    h = PhaseVocoder(1024, TIME_SHIFT, 1.0, 4, mode=REF_COMPAT, max_frames=128)
+    h.set_window(torch.from_numpy(w).cuda())
+    out, _ = h.process(torch.from_numpy(x).cuda())
+    assert rms(out.cpu().numpy()[0], pvref.compat_process(x, 1024, 4, window=w)) <= 1e-5
+    s = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=16)
+    with pytest.raises(Exception):
+        s.set_window(torch.from_numpy(w).cuda())
+    with pytest.raises(Exception):
+        PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, window=_lib.PV_WINDOW_HANN_REF)

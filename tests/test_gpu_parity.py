@@ -244,3 +244,27 @@ def test_run_length_geometries(cuda, monkeypatch, F, effect, scale):
     pv16 = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=440)
     out16, _ = pv16.process(to_dev(xs))
     assert np.abs(out16.cpu().numpy() - g).max() <= 1e-6
+
+
+@pytest.mark.parametrize("n", [1000, 900, 769, 1023])
+def test_short_input_between_n_minus_hop_and_n(cuda, n):
+    """N - hop < n < N: the one frame is partly past the end and must read
+    zeros there (deviation 1), not the samples that follow in memory — with C = 2 and
+    ldx == n those are the next channel's, with C = 1 a sentinel tail placed after n."""
+    import torch
+    N, hop_div = 1024, 4
+    assert N - N // hop_div < n < N
+    xs = np.stack([synth(n, 70), synth(n, 71) + 0.5]).astype(np.float32)
+    pv = PhaseVocoder(N, TIME_SHIFT, 0.5, hop_div, mode=STANDARD, max_channels=2, max_frames=8)
+    assert pv.num_frames(n) == 1
+    out, spec = pv.process(to_dev(xs))                       # ldx == n
+    for c in range(2):
+        ref = pvref.std_process(xs[c], N, hop_div, ord("t"), 0.5)
+        assert rms(out[c].cpu().numpy(), ref) <= RMS_TOL, f"channel {c}"
+        mag, ph = pvref.std_analysis(xs[c], N, N // hop_div, 1)
+        assert np.array_equal(spec[c, 0, :N // 2 + 1, 1].cpu().numpy().view(np.uint32), ph.view(np.uint32))
+    buf = torch.full((N + 64,), 1e3, device="cuda")
+    buf[:n] = to_dev(xs[0])
+    one = PhaseVocoder(N, TIME_SHIFT, 0.5, hop_div, mode=STANDARD, max_frames=8)
+    o1, _ = one.process(buf[:n])
+    assert torch.equal(o1[0], out[0])

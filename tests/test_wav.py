@@ -52,3 +52,20 @@ def test_encode16_truncates_and_clamps():
     assert list(body) == [16383, -16383, 32767, -32767, 0]
     s, _, _ = wav.decode(data)
     assert s.shape == (1, 5)
+
+
+def test_encode16_nan_is_zero():
+    body = np.frombuffer(wav.encode16(np.array([[np.nan, 0.25]]))[44:], "<i2")
+    assert list(body) == [0, 8191]
+
+
+def test_reference_440sine_fixture():
+    """tests/golden/testtones_440sine.wav = the reference's testtones/440sine.wav (config 1
+    input): 441000 frames per the header, the data chunk 2 bytes short (last R missing)."""
+    import os
+    from conftest import GOLDEN
+    data = open(os.path.join(GOLDEN, "testtones_440sine.wav"), "rb").read()
+    s, sr, bits = wav.decode(data)
+    assert s.shape == (2, 441000) and sr == 44100 and bits == 16
+    assert len(data) == 44 + 441000 * 4 - 2 and s[1, -1] == 0.0
+    assert np.array_equal(s[0, :32768], np.load(os.path.join(GOLDEN, "sine440_ch0_32768.npy")))
