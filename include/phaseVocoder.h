@@ -68,8 +68,10 @@ class PhaseVocoder {
 
     // phaseVocoder.h:46-78: hop = samples/2, timeScale 1, periodic Hann
     // imp[i] = 0.5f*(1.f - cosf(2.f*M_PI*i/samples)); the real-time buffers are allocated
-    explicit PhaseVocoder(int samples, int max_frames = PV_DEFAULT_MAX_FRAMES, int device = 0) {
-        init(samples, TIME_SHIFT, 1.0f, 2, PV_MODE_REF_COMPAT, PV_WINDOW_HANN_REF, 1, max_frames, device);
+    explicit PhaseVocoder(int samples, int max_channels = 1, int max_frames = PV_DEFAULT_MAX_FRAMES,
+                          int device = 0) {
+        init(samples, TIME_SHIFT, 1.0f, 2, PV_MODE_REF_COMPAT, PV_WINDOW_HANN_REF, max_channels, max_frames,
+             device);
         std::vector<float> w(2 * (size_t)samples);  // imp1: 2N entries (the reference writes
         for (int i = 0; i < 2 * samples; ++i)          // 2N into an N-float buffer)
             w[i] = 0.5f * (1.f - cosf((float)(2.0 * M_PI * (double)i / (double)samples)));

@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
     const int padN = numSamples + 2 * N;  // frames near the end read zeros (deviation 1)
     const int cap = frames + numSamples / std::max(1, (int)(scale * hop)) + 2;
     std::unique_ptr<PhaseVocoder> owner(
-        single_arg ? new PhaseVocoder(N, cap)                                     // main.cpp:84 analogue
+        single_arg ? new PhaseVocoder(N, numChannels > 0 ? numChannels : 1, cap)  // phaseVocoder.h:46
                    : new PhaseVocoder(N, effect, scale, hopdiv, mode, numChannels > 0 ? numChannels : 1, cap));
     PhaseVocoder& phase = *owner;
     const int outLen = (int)(phase.timeScale * numSamples);
@@ -117,12 +117,14 @@ int main(int argc, char** argv) {
                                       "pv_process", __LINE__);
         HIPCHECK(hipDeviceSynchronize());
         std::vector<float> h((size_t)std::max(olen, 1LL));
-        for (int c = 0; c < numChannels && c < 2; ++c) {
-            HIPCHECK(hipMemcpy(h.data(), d_out + (size_t)c * olen, sizeof(float) * olen, hipMemcpyDeviceToHost));
-            for (int i = 0; i < outLen && i < olen; ++i) outFile[c][i] = h[i];
-            if (c == 0) emitted.assign(h.begin(), h.begin() + std::min<long long>(olen, outLen));
-        }
-        if (numChannels == 1) outFile[1] = outFile[0];
+        // main.cpp:264-297 writes channel 0's first floor(n/outHop)*outHop samples to L and R
+        // (the `numChannels = 1` assignment ends its channel loop); every channel was
+        // processed, as main.cpp analyses every channel
+        const long long n_emit = std::min<long long>((long long)(numSamples / phase.outHopSize) * phase.outHopSize,
+                                                     std::min<long long>(olen, outLen));
+        HIPCHECK(hipMemcpy(h.data(), d_out, sizeof(float) * olen, hipMemcpyDeviceToHost));
+        for (long long i = 0; i < n_emit; ++i) outFile[0][i] = outFile[1][i] = h[i];
+        emitted.assign(h.begin(), h.begin() + n_emit);
         HIPCHECK(hipFree(d_spec));
         HIPCHECK(hipFree(d_out));
     } else {

@@ -231,3 +231,25 @@ def test_python_mirror_single_arg_and_set_window(cuda):
         s.set_window(torch.from_numpy(w).cuda())
     with pytest.raises(Exception):
         PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, window=_lib.PV_WINDOW_HANN_REF)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_gpu_reproduces_reference_output_testout_wav(cuda, tmp_path, batched):
+    """The reference's own output artifact: output/testout.wav = main.cpp
+    (PhaseVocoder(256, 't', 1, 2)) on testtones/test.wav.  The GPU driver's 16-bit WAV is
+    within 1 LSB of it at every sample, and >= 99.9 % bit-identical
+    (tests/golden/make_reference_artifacts.py; the oracle pin is
+    tests/test_oracle.py::test_oracle_reproduces_reference_output_testout_wav)."""
+    x = np.load(os.path.join(GOLDEN, "ref_test_wav_ch0_int16.npy")).astype(np.float32) / np.float32(32768.0)
+    ref_out = np.load(os.path.join(GOLDEN, "ref_testout_wav_L_int16.npy")).astype(np.int64)
+    path = str(tmp_path / "test.wav")
+    write_pcm16(path, x)
+    out_wav = str(tmp_path / "testout.wav")
+    run_main([path, "t", out_wav] + (["--batched"] if batched else []))   # main.cpp:84 defaults
+    s, sr, bits = wav.load(out_wav)
+    assert s.shape == (2, 441000) and bits == 16
+    got = np.round(s[0].astype(np.float64) * 32768).astype(np.int64)
+    d = got - ref_out
+    assert np.abs(d).max() <= 1
+    assert np.mean(d == 0) >= 0.999
+    assert np.array_equal(s[0], s[1])
