@@ -243,17 +243,23 @@ def main():
                 traffic = tj.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
-    # the box's measured HBM ceilings (scripts/bw_probe.hip -> profiles/r01_bw_probe.jsonl):
-    # the 8 TB/s peak is the spec figure; copy streams reach ~4.8 TB/s on MI355X
+    # the box's measured HBM ceilings (scripts/bw_probe.hip -> profiles/r02_bw_probe.jsonl,
+    # random data, several accesses in flight per lane): the 8 TB/s peak is the spec figure;
+    # plain streams reach ~6 TB/s, and the analysis kernel's own byte mix and store shape
+    # with no arithmetic at all (ana_mix_nt) runs at ~4.8 TB/s on MI355X
     ceiling = None
-    probe = os.path.join(ROOT, "profiles", "r01_bw_probe.jsonl")
+    probe = os.path.join(ROOT, "profiles", "r02_bw_probe.jsonl")
     if os.path.exists(probe):
         try:
             rows = {d["probe"]: d["GBps"] for d in map(json.loads, open(probe)) if d}
             copy = max(v for k, v in rows.items() if k.startswith("copy"))
-            ceiling = {"copy_GBps": copy, "frac_of_copy": achieved / copy,
+            write = max(v for k, v in rows.items() if k.startswith("write"))
+            ceiling = {"copy_GBps": copy, "write_GBps": write, "frac_of_copy": achieved / copy,
                        "traffic_frac_of_copy": (traffic / (avg_ms * 1e-3) / 1e9 / copy) if traffic else None,
-                       "source": "profiles/r01_bw_probe.jsonl"}
+                       "source": "profiles/r02_bw_probe.jsonl"}
+            pat = {"analysis": "ana_mix_nt", "synthesis": "syn_mix"}.get(dom)
+            if pat in rows and wl == "c3":
+                ceiling.update(pattern=pat, pattern_GBps=rows[pat], frac_of_pattern=achieved / rows[pat])
         except Exception:
             ceiling = None
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}

@@ -102,7 +102,12 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
         constexpr bool HALO = decltype(halo_tag)::value;
         float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
         (void)srow;
+#ifdef PV_ABL_NOFFT  // timing-only ablation: the tile holds the windowed input, no FFT
+        pass_store<L, Geo<L>::NPASS - 1>(z, tile, lane);
+        wave_lds_sync();
+#else
         fft_run<L, false>(z, tile, twl, tw0, lane);
+#endif
         // bins in chunks of CH (bounded live registers), all reads of a chunk batched
         constexpr int CH = PV_ANA_CH;
 #pragma unroll
@@ -114,7 +119,11 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
                 const int i = i0 + c2;
                 if (i > E) break;
                 const int k = (i == E) ? L : lane + 64 * i;
+#ifdef PV_ABL_NOATAN  // timing-only ablation: no atan2 (phases wrong)
+                const float ph = X[c2].y;
+#else
                 const float ph = atan2_pv(X[c2].y, X[c2].x);
+#endif
                 if constexpr (!HALO) {
                     // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
                     // the phase, which drives the unwrap decisions, stays bit-exact
@@ -134,6 +143,9 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
                         __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
                     }
 #elif PV_NT_SPEC
+#ifdef PV_ABL_NOSTORE  // timing-only ablation: the stores never execute (p.frames > 0)
+                    if (p.frames < 0)
+#endif
                     __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
 #else
                     srow[(i == E) ? L - lane : 64 * i] = make_float2(mag, ph);
@@ -179,6 +191,12 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
         frame(-1, z, std::true_type{});
     }
     const int ufast = (int)min((long long)nfr, max(0LL, lastfull - t0 + 1));
+#ifdef PV_CLOCK_PROBE
+    // diagnostic build only (MI355X_MICROARCH.md DVFS item 6): shader-clock ticks and
+    // 100 MHz real-time ticks around the frame loop; clock = dmemtime / drealtime * 100 MHz
+    const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // steady state, trip u: [load x(u+1)] [compute frame u: E + 1 row stores]
     // [vmcnt(E + 1): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
     // The prefetch index is clamped (the last trip reloads its own frame), so the loads
@@ -235,6 +253,15 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
         frame(u, z, std::false_type{});
     }
     if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = -(int)sacc[i]; })
+#ifdef PV_CLOCK_PROBE
+    const unsigned long long clk_c1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long clk_r1 = __builtin_amdgcn_s_memrealtime();
+    if (p.clk != nullptr && lane == 0) {
+        const long long wv = (long long)c * p.nruns + run;
+        p.clk[2 * wv] = clk_c1 - clk_c0;
+        p.clk[2 * wv + 1] = clk_r1 - clk_r0;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT

@@ -112,6 +112,7 @@ struct pv_handle {
     // workspace
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
+    unsigned long long* d_clk = nullptr;  // PV_CLOCK_PROBE builds only
     Profile prof;
 };
 
@@ -202,6 +203,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.runsum = want_runsum ? h->d_runsum : nullptr;
     p.bins_pad = h->bins_pad;
     p.nan_faithful = h->nan_faithful;
+    p.clk = h->d_clk;
     if (h->mode == PV_MODE_STANDARD)
         PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
     else
@@ -346,7 +348,7 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails};
+                    h->d_carry, h->d_tails, h->d_clk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
@@ -529,6 +531,10 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
     }
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
+#ifdef PV_CLOCK_PROBE
+    PV_HIP(hipMalloc((void**)&h->d_clk, sizeof(unsigned long long) * 2 * runs_total));
+    PV_HIP(hipMemset(h->d_clk, 0, sizeof(unsigned long long) * 2 * runs_total));
+#endif
 
     // LDS budget check for the synthesis kernel (largest)
     size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->hs);
@@ -662,6 +668,16 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
     PV_HIP(hipStreamSynchronize(s));
     return PV_OK;
 }
+
+#ifdef PV_CLOCK_PROBE
+// diagnostic builds only (not declared in pv.h): the per-wave {memtime, realtime} deltas
+// of the last analysis launch, 2 * channels * runs values
+pv_status pv_debug_clock(pv_handle* h, unsigned long long* host, size_t n) {
+    if (!h || !host || !h->d_clk) return fail(PV_ERR_ARG, "no clock buffer");
+    PV_HIP(hipMemcpy(host, h->d_clk, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return PV_OK;
+}
+#endif
 
 pv_status pv_set_window(pv_handle* h, const float* win, void* stream) {
     if (!h || !win) return fail(PV_ERR_ARG, "null argument");

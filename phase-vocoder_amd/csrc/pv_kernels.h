@@ -21,6 +21,7 @@ struct AnaParams {
     int* runsum;            // [C][nruns][2][bins_pad] {S, m0} or nullptr
     int bins_pad;
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
+    unsigned long long* clk;  // PV_CLOCK_PROBE diagnostic builds: per wave {memtime, realtime} deltas
 };
 
 struct ScanParams {

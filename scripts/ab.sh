@@ -11,7 +11,7 @@ fi
 for rep in 1 2; do
   for n in base "${names[@]}"; do
     if [ "$n" = base ]; then lib=phase-vocoder_amd/build/libpv.so; else lib=phase-vocoder_amd/build/variants/libpv_$n.so; fi
-    PV_LIB_PATH=$PWD/$lib timeout -k 10 240 python bench.py --no-cpu --steps ${AB_STEPS:-10} ${AB_ARGS:-} > gpurun_out/ab/$n.$rep.log 2>&1
+    PV_LIB_PATH=$PWD/$lib timeout -k 10 240 python bench.py --no-cpu --no-check --steps ${AB_STEPS:-10} ${AB_ARGS:-} > gpurun_out/ab/$n.$rep.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "$n rc=$rc"; tail -3 gpurun_out/ab/$n.$rep.log; exit $rc; fi
     python3 -c "
