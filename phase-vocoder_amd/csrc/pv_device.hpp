@@ -301,6 +301,30 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // ------------------------------------------------------------------ FFT geometry
+// LDS tile layouts.  A frame's tile carries NPASS - 1 inter-pass exchanges (pass P stores,
+// pass P + 1 loads) and the final natural-order image (last pass stores; the real split,
+// the synthesis' time samples and the FFT op read it).  Each has its own layout, chosen by
+// a bank-conflict model of its exact access shapes (MI355X_MICROARCH.md §LDS: ds_read_b64
+// in 2 x 32 lanes over 64 banks, ds_write_b64 in 4 x 16 lanes over 32 banks):
+//   exchange X: slot(p) = p + XC * (p >> XS)   (XC pad slots every 2^XS points)
+//   final image: slot(p) = p                   (contiguous and mirrored 32-lane reads and
+//                                               the last pass's contiguous stores are all
+//                                               conflict-free unpadded)
+// At L = 512 this is 176 LDS-array cycles per frame-transform instead of 256 with one pad
+// every E points for every image.  Every access is still one per-lane base plus
+// compile-time offsets: slot(a + c) = slot(a) + slot(c) for all (a, c) the passes use.
+constexpr int lay_c(int L, int X) {
+    return L == 128 ? (X == 0 ? 1 : X == 1 ? 2 : X == 2 ? 4 : X == 3 ? 8 : 0)
+         : L == 256 ? (X == 0 ? 1 : X == 1 ? 4 : 0)
+         : L == 512 ? (X == 0 ? 1 : X == 1 ? 8 : 0)
+         : L == 1024 ? (X == 0 ? 1 : 0)
+         : (X == 0 ? 1 : 0);
+}
+constexpr int lay_s(int L, int X) {
+    return L == 512 && X == 1 ? 6 : L == 2048 ? 5 : 4;
+}
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
 template <int L_>
 struct Geo {
     static constexpr int L = L_;
@@ -308,14 +332,52 @@ struct Geo {
     static constexpr int E = L / 64;                 // complex points per lane
     static constexpr int RLOG = ilog2c(E);           // stages per full pass
     static constexpr int NPASS = (LOG2L + RLOG - 1) / RLOG;
-    static constexpr int PADSH = RLOG;               // one pad slot every E points
-    static constexpr int TILE = L + (L >> PADSH) + 2;  // padded LDS tile (float2), +bin L
     static_assert(L >= 128 && L <= 2048, "one frame per wave: L in [128, 2048]");
-    __device__ static __forceinline__ int pad(int p) { return p + (p >> PADSH); }
-    // pad(a + c) = pad(a) + padc(c) whenever c or a is a multiple of E (all access
-    // patterns below): one per-lane base address plus a compile-time offset.
-    static constexpr int padc(int c) { return c + (c >> PADSH); }
+    // exchange X's slot of point p (constexpr: offsets fold into the instruction)
+    template <int X>
+    __host__ __device__ static constexpr int xslot(int p) {
+        return p + lay_c(L, X) * (p >> lay_s(L, X));
+    }
+    static constexpr int xsize(int X) { return (L - 1) + lay_c(L, X) * ((L - 1) >> lay_s(L, X)) + 1; }
+    static constexpr int max_xsize() {
+        int m = L;
+        for (int X = 0; X + 1 < NPASS; ++X) m = cmax(m, xsize(X));
+        return m;
+    }
+    static constexpr int TILE = max_xsize() + 2;  // LDS tile (float2), +bin L
+    // every exchange layout must keep "per-lane base + compile-time offset" exact for the
+    // address pairs pass_store / pass_load form (checked at compile time below)
+    static constexpr bool layouts_affine() {
+        for (int P = 0; P + 1 < NPASS; ++P) {
+            const int S = 1 << (P * RLOG);
+            const int r = cmin(RLOG, LOG2L - P * RLOG), R = 1 << r;
+            const int r2 = cmin(RLOG, LOG2L - (P + 1) * RLOG), R2 = 1 << r2;
+            const int c = lay_c(L, P), s = lay_s(L, P);
+            auto sl = [&](int p) { return p + c * (p >> s); };
+            for (int j = 0; j < L / R; ++j) {
+                const int J = (j / S) * R * S + (j & (S - 1));
+                for (int f = 0; f < R; ++f) {
+                    const int off = S * bitrevc(f, r);
+                    if (sl(J + off) != sl(J) + sl(off)) return false;
+                }
+            }
+            for (int lane = 0; lane < 64; ++lane)
+                for (int g = 0; g < E / R2; ++g)
+                    for (int q = 0; q < R2; ++q) {
+                        const int off = 64 * g + q * (L / R2);
+                        if (sl(lane + off) != sl(lane) + sl(off)) return false;
+                    }
+        }
+        return true;
+    }
+
+    // final natural-order image: unpadded
+    __device__ static __forceinline__ int pad(int p) { return p; }
+    static constexpr int padc(int c) { return c; }
 };
+static_assert(Geo<128>::layouts_affine() && Geo<256>::layouts_affine() && Geo<512>::layouts_affine() &&
+                  Geo<1024>::layouts_affine() && Geo<2048>::layouts_affine(),
+              "tile layout breaks base + offset addressing");
 
 // Stage-major twiddle table: stage Ns occupies [Ns-1, 2Ns-1), entry idx = e^{-i pi idx/Ns}
 // (the values of the oracle's master table tw[idx*L/(2Ns)], copied, so bit-identical).
@@ -400,9 +462,14 @@ __device__ __forceinline__ void pass_store(const float2 (&v)[Geo<L>::E], float2*
     for (int g = 0; g < NG; ++g) {
         const int j = lane + 64 * g;
         const int J = (j / S) * R * S + (j & (S - 1));
-        float2* base = tile + G_::pad(J);  // J = 0 mod E when S = 1; S*br = 0 mod E when S >= E
+        // inter-pass exchange P, or the final image after the last pass
+        constexpr bool FIN = (P + 1 == G_::NPASS);
+        float2* base = tile + (FIN ? J : G_::template xslot<(FIN ? 0 : P)>(J));
 #pragma unroll
-        for (int f = 0; f < R; ++f) base[G_::padc(S * bitrevc(f, r))] = v[g * R + f];
+        for (int f = 0; f < R; ++f) {
+            const int off = S * bitrevc(f, r);
+            base[FIN ? off : G_::template xslot<(FIN ? 0 : P)>(off)] = v[g * R + f];
+        }
     }
 }
 
@@ -412,11 +479,12 @@ __device__ __forceinline__ void pass_load(float2 (&v)[Geo<L>::E], const float2* 
     constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
     constexpr int R = 1 << r;
     constexpr int NG = G_::E / R;
-    const float2* base = tile + G_::pad(lane);
+    static_assert(P >= 1, "pass 0 reads registers");
+    const float2* base = tile + G_::template xslot<P - 1>(lane);  // exchange P - 1
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
-        for (int q = 0; q < R; ++q) v[g * R + q] = lds_ld(&base[G_::padc(64 * g + q * (L / R))]);
+        for (int q = 0; q < R; ++q) v[g * R + q] = lds_ld(&base[G_::template xslot<P - 1>(64 * g + q * (L / R))]);
     }
 }
 
