@@ -24,6 +24,9 @@
 #ifndef PV_ANA_SHIFT
 #define PV_ANA_SHIFT 1  // shifted-register input when hop = 128 D (k_std_analysis<L, false, D>)
 #endif
+#ifndef PV_ANA_PF2
+#define PV_ANA_PF2 0  // analysis input prefetch distance 2 (shifted-register path)
+#endif
 #ifndef PV_ANA_CH
 #define PV_ANA_CH 3  // analysis: bins per batch of LDS reads + atan2 chains
 #endif
@@ -201,7 +204,43 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     // [vmcnt(E + 1): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
     // The prefetch index is clamped (the last trip reloads its own frame), so the loads
     // and stores are unconditional and the count is exact (gload_pairs / vm_wait).
-    if constexpr (D > 0) {
+    if constexpr (D > 0 && PV_ANA_PF2 && 2 * (E + 1) + D <= 63) {  // vmcnt holds 6 bits
+        // prefetch distance 2: the wait for x(u+1) (issued at the top of trip u-1, before
+        // frame u-1's row stores) no longer has to drain frame u-1's stores (vmcnt counts in
+        // issue order), so a frame's stores stay in flight for two trips.  Unrolled by two so
+        // the two in-flight buffers never move.
+        static_assert(D < E, "shifted input: hop < N / 2");
+        if (ufast > 0) {
+            float2 xr[E], z[E];
+            load_fast(0, xr);
+            window(xr, z);
+            f2v xa[D], xb[D];
+            gload_tail<D, E>(xa, xc + (long long)(t0 + min(1, ufast - 1)) * p.hop + 2 * lane);
+            auto shift_in = [&](f2v (&xv)[D]) {
+#pragma unroll
+                for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) xr[E - D + j] = make_float2(xv[j].x, xv[j].y);
+                window(xr, z);
+            };
+            int u = 0;
+            for (; u + 1 < ufast; u += 2) {
+                gload_tail<D, E>(xb, xc + (long long)(t0 + min(u + 2, ufast - 1)) * p.hop + 2 * lane);
+                frame(u, z, std::false_type{});
+                // x(u+1): frame u-1's and u's stores may stay in flight (the first pair has
+                // no frame u-1 stores between xa and xb, so its count is E + 1 smaller)
+                if (u == 0) vm_wait<(E + 1) + D>(xa);
+                else vm_wait<2 * (E + 1) + D>(xa);
+                shift_in(xa);
+                gload_tail<D, E>(xa, xc + (long long)(t0 + min(u + 3, ufast - 1)) * p.hop + 2 * lane);
+                frame(u + 1, z, std::false_type{});
+                vm_wait<2 * (E + 1) + D>(xb);
+                shift_in(xb);
+            }
+            if (u < ufast) frame(u, z, std::false_type{});  // odd count: the last frame
+            vm_wait<0>(xa);  // xa's (clamped) prefetch lands before its registers are reused
+        }
+    } else if constexpr (D > 0) {
         static_assert(D < E, "shifted input: hop < N / 2");
         if (ufast > 0) {
             float2 xr[E], z[E];
