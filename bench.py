@@ -228,7 +228,9 @@ def main():
     hop_a, hop_s, B = N // hop_div, pv.outHopSize, N // 2 + 1
     per_frame = {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
                  "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
-                 "carry": 0, "runsum": 8 * B, "seam": 0}
+                 "carry": 0, "runsum": 8 * B, "seam": 0,
+                 # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
+                 "fused": 4 * hop_a + 8 * B + 4 * hop_s}
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     avg_ms = ms_tot / max(launches, 1)

@@ -38,10 +38,10 @@ pv_status fail(pv_status s, const std::string& msg) {
     } while (0)
 
 constexpr double kPi = 3.14159265358979323846;
-constexpr int kNumKernels = 7;
+constexpr int kNumKernels = 8;
 const char* kKernelNames[kNumKernels] = {"analysis", "runsum", "carry", "synthesis",
-                                         "seam", "compat_analysis", "rt"};
-enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5, KRT = 6 };
+                                         "seam", "compat_analysis", "rt", "fused"};
+enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5, KRT = 6, KF = 7 };
 
 bool is_pow2(long long v) { return v > 0 && (v & (v - 1)) == 0; }
 
@@ -100,6 +100,7 @@ struct pv_handle {
     pv_config cfg{};
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
+    int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
@@ -112,6 +113,7 @@ struct pv_handle {
     // workspace
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
+    int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
     unsigned long long* d_clk = nullptr;  // PV_CLOCK_PROBE builds only
     Profile prof;
 };
@@ -297,6 +299,50 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     return PV_OK;
 }
 
+// q = 1 (STANDARD): analysis, processing, resynthesis and every seam in one launch
+// (pv_fused.hip); outputs equal to do_analysis + do_resynthesis (bit for bit at equal F)
+pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int C, int frames,
+                   pv_float2* spec, long long ld_spec, float* out, long long ldo, hipStream_t s) {
+    if (C == 0 || frames == 0) return PV_OK;
+    if (!x || !spec || !out) return fail(PV_ERR_ARG, "null x/spec/out");
+    if (ld_spec < (long long)frames * h->spec_stride)
+        return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
+    if (C > 1 && ldx < n) return fail(PV_ERR_ARG, "ldx < n_samples");
+    const long long olen = pv_output_length(h, frames);
+    if (C > 1 && ldo < olen) return fail(PV_ERR_ARG, "ldo < pv_output_length");
+    const int F = h->F_fused;
+    const int nruns = (frames + F - 1) / F;
+    pv::FusedParams p{};
+    p.x = x;
+    p.ldx = ldx;
+    p.n = n;
+    p.hop = h->hop;
+    p.frames = frames;
+    p.F = F;
+    p.nruns = nruns;
+    p.aligned = (((uintptr_t)x & 7) == 0) && (ldx % 2 == 0) && (h->hop % 2 == 0);
+    p.win = h->d_win;
+    p.tw = h->d_tw_syn;    // the stage-major L-point table serves both directions
+    p.tws = h->d_tws_syn;  // e^{-2 pi i k/N}, k <= N/2: the analysis split's table too
+    p.src_first = h->d_src_first;
+    p.src_cnt = h->d_src_cnt;
+    p.rho = h->rho;
+    p.gain = h->d_gain;
+    p.hs = h->hs;
+    p.spec = reinterpret_cast<float2*>(spec);
+    p.ld_spec = ld_spec;
+    p.spec_stride = h->spec_stride;
+    p.out = out;
+    p.ldo = ldo;
+    p.out_len = olen;
+    p.out_aligned = ((reinterpret_cast<uintptr_t>(out) & 7) == 0) && ((ldo & 1) == 0);
+    p.tails = h->d_tails;
+    p.tail_len = h->tail_len;
+    p.seam_flags = h->d_seam_flags;
+    PV_LAUNCH(h, KF, s, pv::launch_fused(h->L_syn, h->pitch ? 2 : 0, C, p, s));
+    return PV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -348,7 +394,7 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails, h->d_clk};
+                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_clk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
@@ -522,15 +568,34 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if ((st = upload(&h->d_src_first, first)) != PV_OK) return bail(st);
     if ((st = upload(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
 
+    // ---- single-launch path (q = 1): no halo frame, so runs can be as short as the overlap
+    // tail allows (F hs >= N - hs) to give a single stream enough waves; PV_FUSED=0 disables
+    // it (A/B), PV_FUSED_FRAMES overrides its run length
+    if (h->mode == PV_MODE_STANDARD && h->q == 1 && pv::fused_supported(h->L_syn, h->hs)) {
+        const int fmin = std::max(2, (h->tail_len + h->hs - 1) / h->hs);
+        int Ff = (int)std::min<long long>(h->F, std::max<long long>(fmin, work / 4096));
+        if (const char* ev = std::getenv("PV_FUSED_FRAMES")) {
+            const int f = std::atoi(ev);
+            if (f >= fmin && f <= 256) Ff = f;
+        }
+        const char* en = std::getenv("PV_FUSED");
+        if (!(en && en[0] == '0')) h->F_fused = Ff;
+    }
+    const int runs_fused = h->F_fused > 0 ? (cfg->max_frames + h->F_fused - 1) / h->F_fused : 0;
+
     // ---- workspace
     const size_t chans = (size_t)std::max(cfg->max_channels, 1);
     const size_t runs_total = chans * std::max(h->max_runs, 1);
-    const size_t wg_total = chans * std::max((h->max_runs + 3) / 4, 1);
+    const size_t wg_total = chans * std::max((std::max(h->max_runs, runs_fused) + 3) / 4, 1);
     if (h->mode == PV_MODE_STANDARD) {
         PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * 2 * h->bins_pad));
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
     }
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
+    if (h->F_fused > 0) {
+        PV_HIP(hipMalloc((void**)&h->d_seam_flags, sizeof(int) * wg_total));
+        PV_HIP(hipMemset(h->d_seam_flags, 0, sizeof(int) * wg_total));
+    }
 #ifdef PV_CLOCK_PROBE
     PV_HIP(hipMalloc((void**)&h->d_clk, sizeof(unsigned long long) * 2 * runs_total));
     PV_HIP(hipMemset(h->d_clk, 0, sizeof(unsigned long long) * 2 * runs_total));
@@ -569,6 +634,7 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     if (st != PV_OK) return st;
     DeviceGuard g(h->cfg.device);
     hipStream_t s = (hipStream_t)stream;
+    if (h->F_fused > 0) return do_fused(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
     if (st != PV_OK) return st;

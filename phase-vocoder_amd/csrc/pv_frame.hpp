@@ -146,8 +146,12 @@ struct NoHook {
 };
 // hook(): called once the spectrum row sv has been consumed (before the inverse real-FFT
 // pre-step) — the batched kernel issues the next row's loads there into the same registers.
+// Q1: the output-phase denominator is q = 1 (integer ratio, e.g. pitch 2.0): the unwrap
+// count drops out of the output phase (rho phi + 2 pi ((p M) mod 1) = rho phi), so the
+// unwrap state is neither read nor updated; phc = fma(rho / 2 pi, phi, +0) is bit for bit
+// what the RACC path computes with q = 1 (R = tj = +0).
 template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false,
-          typename Hook = NoHook>
+          bool Q1 = false, typename Hook = NoHook>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
@@ -172,12 +176,16 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         float phc[E + 1];
         float ekv[E + 1];
         unsigned jkv[E + 1];
-        if constexpr (KREG) {
+        if constexpr (Q1) {
+            (void)ekv; (void)jkv;
+        } else if constexpr (KREG) {
             PV_FOR_BINS(E, lane, { ekv[i] = ekr[i]; jkv[i] = jkr[i]; })
         } else {
             PV_FOR_BINS(E, lane, { ekv[i] = lds_ld(&ekl[k]); jkv[i] = lds_ld(&jkl[k]); })
         }
-        if constexpr (RACC) {
+        if constexpr (Q1) {
+            PV_FOR_BINS(E, lane, { phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], 0.0f); })
+        } else if constexpr (RACC) {
             const float npq = -pm.p_over_q;  // -(p mod q) / q
             const float tqf = (float)tq;
             PV_FOR_BINS(E, lane, {

@@ -1,0 +1,305 @@
+// pv_fused.hip — analysis -> processing -> resynthesis in ONE launch, for STANDARD
+// configurations whose output phase does not depend on the unwrap count (q = 1: an integer
+// ratio, e.g. BASELINE config 2, pitch 2.0).
+//
+// Why only q = 1: the output phase is rho phi + 2 pi ((p M) mod q) / q,
+// and M, the running unwrap count, needs every earlier frame of the channel — the split
+// path's analysis -> k_carry scan -> synthesis.  With q = 1 the last term is 0, so frame t's
+// output depends on frame t's spectrum alone: a wave can analyse a frame, keep its
+// {mag, phase} row in registers, resynthesise it at once and overlap-add it, with no halo
+// frame, no run records and no second pass over the spectrum.  The spectrum row is still
+// stored (the caller's spectrum buffer is an output of pv_process), but it is
+// never read back: per frame 4 hop_a + 8 (N/2+1) + 4 hop_s bytes instead of the split
+// path's 4 hop_a + 16 (N/2+1) + 4 hop_s, and one launch instead of two (config 2 is a
+// single stream: per-launch costs, not bytes, bound it).
+//
+// The per-frame arithmetic is k_std_analysis's (window, FFT, split, atan2, sqrt) and
+// k_synthesis's (synth_frame, register overlap-add, tails, seams) operation for operation,
+// so the spectrum and the output are bit-identical to the split path (tests/test_gpu_parity.py).
+// Geometry as k_synthesis: a wave = a run of F frames of one channel, 4 runs per workgroup,
+// the intra-workgroup seams closed after one barrier, the inter-workgroup seams by the
+// second of the two workgroups to finish (no k_seam launch).
+#include "pv_frame.hpp"
+#include "pv_kernels.h"
+
+namespace pv {
+
+// Inter-workgroup hand-off without fences (MI355X_MICROARCH.md, "Valid forms": write-through
+// `sc1` stores of every handed-off byte, the storing wave's vmcnt(0) before its counter add,
+// `sc1` loads of them after the add has returned): an agent-scope release/acquire pair
+// would write back / invalidate whole caches (buffer_wbl2 / buffer_inv) per workgroup.
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(float* p, f2v v) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+// counter add after every store of the wave has left (relaxed: the sc1 stores need no fence)
+__device__ __forceinline__ int arrive(int* flag, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __shfl(old, 0);
+}
+
+template <int L>
+struct FuGeo {
+    static constexpr int N = 2 * L;
+    static constexpr int B = L + 1;
+    // float offsets
+    static constexpr int O_TW = 0;                            // L float2
+    static constexpr int O_TWS = O_TW + 2 * L;                // L+1 float2 (+1 pad)
+    static constexpr int O_TILE = O_TWS + 2 * (L + 2);        // 4 x TILE float2
+    static constexpr int O_WIN = O_TILE + 2 * 4 * Geo<L>::TILE;  // N
+    static constexpr int O_SRC = O_WIN + N;                   // 2B (+2) {first, count}
+    static constexpr int FLOATS = O_SRC + 2 * B + 2;
+    static constexpr size_t BYTES = sizeof(float) * FLOATS;
+    static_assert(O_SRC % 2 == 0 && O_TILE % 4 == 0, "alignment of the LDS carve-up");
+};
+
+template <int L, int MODE, int DT>
+__global__ __launch_bounds__(256) void k_fused(FusedParams p) {
+    using G_ = Geo<L>;
+    using FG = FuGeo<L>;
+    constexpr int E = G_::E;
+    constexpr int N = FG::N;
+    constexpr int B = FG::B;
+    constexpr int NS = E;  // overlap-add slots: positions u*hs + 128 s + 2 lane + {0,1}
+    constexpr int D = DT;  // slots completed per frame (out hop = 128 DT)
+    static_assert(DT == 1 || DT == 2 || DT == 4, "register overlap-add");
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    float2* twl = reinterpret_cast<float2*>(fsm + FG::O_TW);
+    float2* twsl = reinterpret_cast<float2*>(fsm + FG::O_TWS);
+    float2* tiles = reinterpret_cast<float2*>(fsm + FG::O_TILE);
+    float* winl = fsm + FG::O_WIN;
+    int* srcl = reinterpret_cast<int*>(fsm + FG::O_SRC);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
+    float2 tw0[E];
+    load_tw0<L>(tw0, p.tw);
+    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
+    for (int i = tid; i < B; i += 256) {
+        twsl[i] = p.tws[i];
+        if (MODE == 2) { srcl[2 * i] = p.src_first[i]; srcl[2 * i + 1] = p.src_cnt[i]; }
+    }
+    for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
+    float2 gn[NS];  // synthesis gains of the lane's OLA slots (frame-invariant)
+    {
+        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) gn[s] = g2[64 * s + lane];
+    }
+    __syncthreads();
+
+    const int c = blockIdx.y;
+    const int run = blockIdx.x * 4 + w;
+    const int t0 = run * p.F;
+    const int nfr = max(0, min(p.F, p.frames - t0));  // real frames of this wave's run
+    const int hs = p.hs;
+    const int TL = N - hs;
+    float2* tile = tiles + w * G_::TILE;
+    const float* xc = p.x + (long long)c * p.ldx;
+    float2* specc = p.spec + (long long)c * p.ld_spec;
+    float* outc = p.out + (long long)c * p.ldo;
+    const long long obase = (long long)t0 * hs;
+
+    // synth_frame's unwrap state and tables are not used with Q1
+    int M[E + 1];
+    float phprev[E + 1];
+    float ekr[E + 1];
+    unsigned jkr[E + 1];
+    const PhaseMap pmap{p.rho * kInv2Pi, 1u, 0u, 1, 1.0f, 0.0f};
+    const SynLds stb{twl, twsl, nullptr, nullptr, srcl};
+
+    float2 acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = make_float2(0.0f, 0.0f);
+
+    // input frame t: samples t*hop + 2 (lane + 64 q) + {0,1}; frames whose N samples are all
+    // inside [0, n) use vector loads, the last N/hop of a channel the bounds-checked path
+    const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
+    auto load = [&](int t, float2 (&xr)[E]) {
+        const long long base = (long long)t * p.hop;
+        if (t <= lastfull) {
+#pragma unroll
+            for (int q = 0; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(xc + base + 2 * (lane + 64 * q));
+        } else {
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const long long s = base + 2 * (lane + 64 * q);
+                xr[q].x = (s < p.n) ? xc[s] : 0.0f;
+                xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
+            }
+        }
+    };
+
+    float2 xr[E];
+    if (nfr > 0) load(t0, xr);
+    for (int u = 0; u < p.F; ++u) {
+        const int t = t0 + u;
+        if (u < nfr) {
+            float2 z[E];
+            {
+                const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    const float2 wv = lds_ld(&wl[64 * q]);
+                    z[q].x = xr[q].x * wv.x;
+                    z[q].y = xr[q].y * wv.y;
+                }
+            }
+            if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
+            // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv
+            fft_run<L, false>(z, tile, twl, tw0, lane);
+            float2 sv[E + 1];
+            float2* srow = specc + (long long)t * p.spec_stride + lane;
+            constexpr int CH = 3;
+#pragma unroll
+            for (int i0 = 0; i0 <= E; i0 += CH) {
+                float2 X[CH];
+                split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
+#pragma unroll
+                for (int c2 = 0; c2 < CH; ++c2) {
+                    const int i = i0 + c2;
+                    if (i > E) break;
+                    const float ph = atan2_pv(X[c2].y, X[c2].x);
+                    float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
+                    sv[i] = make_float2(mag, ph);
+                    // bin L (i = E): the same value and address on every lane
+                    __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+                }
+            }
+            wave_lds_sync();  // split reads done before the synthesis reuses the tile
+            // ---- processing + resynthesis: inverse FFT's last-pass registers
+            synth_frame<L, MODE, false, true, false, false, true>(sv, false, 0u, M, phprev, pmap, stb, tw0, tile,
+                                                                  lane, z, ekr, jkr);
+            // ---- windowed overlap-add in registers
+#pragma unroll
+            for (int idx = 0; idx < E; ++idx) {
+                const int cs = last_slot<L>(idx);
+                acc[cs].x = __builtin_fmaf(z[idx].x, gn[cs].x, acc[cs].x);
+                acc[cs].y = __builtin_fmaf(z[idx].y, gn[cs].y, acc[cs].y);
+            }
+        }
+        // positions [u*hs, (u+1)*hs) = slots 0..D-1 are final — except a workgroup's head
+        // (wave 0, positions < N - hs), which the previous workgroup's tail still overlaps:
+        // those go out write-through for the seam hand-off below
+        const long long pb = obase + (long long)u * hs + 2 * lane;
+        const bool head = (w == 0) && (blockIdx.x > 0) && (u * hs < TL);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const long long gp = pb + 128 * d;
+            if (p.out_aligned && gp + 1 < p.out_len) {
+                if (head) st_sc1(outc + gp, f2v{acc[d].x, acc[d].y});
+                else __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
+            } else if (head) {
+                if (gp < p.out_len) st_sc1(outc + gp, acc[d].x);
+                if (gp + 1 < p.out_len) st_sc1(outc + gp + 1, acc[d].y);
+            } else {
+                if (gp < p.out_len) outc[gp] = acc[d].x;
+                if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
+    }
+    // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
+    __syncthreads();
+    float* rings = reinterpret_cast<float*>(tiles);
+    float* ring = rings + w * N;
+    {
+        float2* r2 = reinterpret_cast<float2*>(ring);
+#pragma unroll
+        for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
+    }
+    __syncthreads();
+    // seams: run w's tail overlaps run w+1's head
+    if (w > 0) {
+        const float* prev = rings + (w - 1) * N;
+        for (int j = lane; j < TL; j += 64) {
+            const long long gp = obase + j;
+            if (gp < p.out_len) outc[gp] += prev[j];
+        }
+    }
+    // Inter-workgroup seam b (workgroup b-1's last tail overlaps workgroup b's head, which
+    // wave 0 of workgroup b stored as if final): closed in this launch by whichever of the
+    // two sides arrives second.  Each side publishes its part write-through (the tail to
+    // `tails`, the head to `out`), waits for its stores, then adds 1 to the seam's counter;
+    // the side whose add returns 1 reads the other part (sc1 loads), writes head + tail and
+    // resets the counter for the next launch.  Nobody waits for anybody, so there is no
+    // dispatch-order assumption; head + tail is the same float whoever adds it.
+    const int nwg = (p.nruns + 3) / 4;
+    if (w == 3) {
+        const bool last = (blockIdx.x + 1 >= nwg);
+        float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len;
+        const long long nbase = obase + (long long)p.F * hs;  // workgroup b+1's first position
+        for (int j = lane; j < TL; j += 64) {
+            const float v = ring[j];
+            if (last) {
+                const long long gp = nbase + j;
+                if (gp < p.out_len) outc[gp] = v;
+            } else {
+                st_sc1(tdst + j, v);
+            }
+        }
+        if (!last) {
+            int* flag = p.seam_flags + (long long)c * nwg + blockIdx.x;
+            if (arrive(flag, lane) == 1) {  // workgroup b+1's head is in out
+                for (int j = lane; j < TL; j += 64) {
+                    const long long gp = nbase + j;
+                    if (gp < p.out_len) outc[gp] = ld_sc1(outc + gp) + ring[j];
+                }
+                if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (w == 0 && blockIdx.x > 0) {
+        int* flag = p.seam_flags + (long long)c * nwg + (blockIdx.x - 1);
+        if (arrive(flag, lane) == 1) {  // workgroup b-1's tail is in tails
+            const float* tsrc = p.tails + ((long long)c * nwg + (blockIdx.x - 1)) * p.tail_len;
+            for (int j = lane; j < TL; j += 64) {
+                const long long gp = obase + j;
+                if (gp < p.out_len) outc[gp] = ld_sc1(outc + gp) + ld_sc1(tsrc + j);
+            }
+            if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+bool fused_supported(int L, int hs) {
+    return L >= 128 && L <= 512 && hs % 128 == 0 && (hs / 128 == 1 || hs / 128 == 2 || hs / 128 == 4) &&
+           hs <= L;
+}
+
+// mode: 0 STANDARD stretch, 2 STANDARD pitch (q = 1 only; the caller checks)
+hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s) {
+    dim3 grid((p.nruns + 3) / 4, channels);
+    const int dt = p.hs / 128;
+#define PV_FU(LL_, MM_)                                                                                 \
+    switch (dt) {                                                                                       \
+        case 1: hipLaunchKernelGGL((k_fused<LL_, MM_, 1>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
+        case 2: hipLaunchKernelGGL((k_fused<LL_, MM_, 2>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
+        case 4: hipLaunchKernelGGL((k_fused<LL_, MM_, 4>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
+        default: return hipErrorInvalidValue;                                                           \
+    }
+#define PV_FU_L(MM_)                          \
+    switch (L) {                              \
+        case 128: PV_FU(128, MM_); break;     \
+        case 256: PV_FU(256, MM_); break;     \
+        case 512: PV_FU(512, MM_); break;     \
+        default: return hipErrorInvalidValue; \
+    }
+    if (mode == 2) { PV_FU_L(2); } else { PV_FU_L(0); }
+#undef PV_FU_L
+#undef PV_FU
+    return hipGetLastError();
+}
+
+}  // namespace pv

@@ -59,6 +59,31 @@ struct SynParams {
     int tail_len;
 };
 
+// single-launch STANDARD path for q = 1 (pv_fused.hip)
+struct FusedParams {
+    const float* x;
+    long long ldx, n;
+    int hop, frames, F, nruns;
+    int aligned;                       // x base, ldx and hop allow 8-byte vector loads
+    const float* win;                  // analysis window (N)
+    const float2* tw;                  // stage-major twiddles, L-point (analysis = synthesis)
+    const float2* tws;                 // e^{-2 pi i k/N}, k <= L
+    const int* src_first;              // pitch map
+    const int* src_cnt;
+    float rho;
+    const float* gain;                 // synthesis window * norm / N   (N)
+    int hs;                            // out hop
+    float2* spec;
+    long long ld_spec;
+    int spec_stride;
+    float* out;
+    long long ldo, out_len;
+    int out_aligned;
+    float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
+    int tail_len;
+    int* seam_flags;                   // [C][nwg] arrival counters, 0 between launches
+};
+
 struct SeamParams {
     float* out;
     long long ldo, out_len;
@@ -114,6 +139,8 @@ hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
+bool fused_supported(int L, int hs);
+hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s);
 size_t synthesis_lds_bytes(int L, int hs);
 hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
                       hipStream_t s);

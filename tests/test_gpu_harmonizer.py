@@ -28,7 +28,7 @@ def rms(a, b):
 
 @pytest.mark.parametrize("N,ratios", [(1024, [1.25, 1.5, 0.75]), (512, [2.0, 1.0]),
                                       (2048, [1.5, 0.5, 1.125, 1.0])])
-def test_harmonizer_voices_and_mix(cuda, N, ratios):
+def test_harmonizer_voices_and_mix(cuda, monkeypatch, N, ratios):
     import torch
     C = 3
     xs = np.stack([synth(40000, 70 + c) for c in range(C)])
@@ -36,6 +36,9 @@ def test_harmonizer_voices_and_mix(cuda, N, ratios):
     gains = [0.5 / (k + 1) for k in range(len(ratios))]
     voices, mix, _ = hz.harmonize(torch.from_numpy(xs).cuda(), gains=gains)
     v = voices.cpu().numpy()
+    # the voices run the split path; a single integer-ratio pv_process would take the fused
+    # launch with its own run length (same values up to the seams, tests/test_gpu_fused.py)
+    monkeypatch.setenv("PV_FUSED", "0")
     for k, r in enumerate(ratios):
         pv = PhaseVocoder(N, PITCH_SHIFT, r, 4, mode=STANDARD, max_channels=C, max_frames=400)
         single, _ = pv.process(torch.from_numpy(xs).cuda())
