@@ -25,13 +25,18 @@ def broadcast_blob(blob, src: int = 0, group=None):
 
 
 def broadcast_tables(pv, src: int = 0, group=None) -> bool:
-    """Rank `src` exports its handle's tables; every other rank imports them.  Returns True
-    when this rank's own tables were already bit-identical to the received ones."""
+    """Rank `src` exports its handle's tables (pv_export_tables: one device blob); every
+    other rank imports them (pv_import_tables).  With the nccl backend (RCCL over xGMI) the
+    device blob is broadcast as is; a CPU backend (gloo: the CPU multi-process tests, a
+    rehearsal on one GPU) stages it through host memory.  Returns True when this rank's own
+    tables were already bit-identical to the received ones."""
     import torch
     import torch.distributed as dist
     mine = pv.export_tables()
-    blob = mine.clone() if dist.get_rank(group) == src else torch.empty_like(mine)
+    wire = mine if dist.get_backend(group) == "nccl" else mine.cpu()
+    blob = wire.clone() if dist.get_rank(group) == src else torch.empty_like(wire)
     broadcast_blob(blob, src=src, group=group)
+    blob = blob.to(mine.device)
     same = bool(torch.equal(blob, mine))
     if dist.get_rank(group) != src:
         pv.import_tables(blob)

@@ -1,0 +1,59 @@
+"""One rank of tests/test_gpu_dist.py (started as a fresh child process per rank; not
+collected by pytest).  gloo process group, the product's table broadcast and its sharded
+pv_process, checked against the oracle.  Prints one JSON line."""
+import json
+import os
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+for p in (os.path.join(ROOT, "phase-vocoder_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+
+def main():
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pvref
+    from pvamd import STANDARD, TIME_SHIFT, PhaseVocoder
+    from pvamd.dist import broadcast_tables, channel_shard
+    from test_gpu_parity import rms, synth
+
+    total, n = int(sys.argv[1]), int(sys.argv[2])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    try:
+        first, count = channel_shard(total, world, rank)
+        xs = np.stack([synth(n, 20240 + c) for c in range(first, first + count)])
+        pv = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_channels=count,
+                          max_frames=pv_frames(n))
+        if rank != 0:  # prove the import takes effect: start from damaged tables
+            bad = pv.export_tables()
+            bad[256:512] ^= 0x5A
+            pv.import_tables(bad)
+        same = broadcast_tables(pv, src=0)
+        out, _ = pv.process(torch.from_numpy(xs).cuda())
+        g = out.cpu().numpy()
+        ref, _ = pvref.std_process_batch(xs, 1024, 4, ord("t"), 0.5)
+        errs = [rms(g[c], ref[c]) for c in range(count)]
+        # the tables every rank now holds are rank 0's, byte for byte
+        tb = pv.export_tables().cpu()
+        allt = [torch.empty_like(tb) for _ in range(world)]
+        dist.all_gather(allt, tb)
+        equal = all(torch.equal(allt[0], t) for t in allt)
+        t = torch.tensor([float(max(errs))], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        print(json.dumps({"rank": rank, "first": first, "count": count, "same_before": same,
+                          "rms": errs, "rms_max_all_ranks": float(t), "tables_equal": equal,
+                          "finite": bool(np.isfinite(g).all())}), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def pv_frames(n, hop=256):
+    return max(1, -(-(n - hop) // hop))
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pvamd.dist import broadcast_blob, channel_shard
+from pvamd.dist import broadcast_blob, broadcast_tables, channel_shard
 
 
 def _free_port():
@@ -61,3 +61,42 @@ def test_channel_shard_uneven():
     assert parts == [(0, 3), (3, 3), (6, 2), (8, 2)]
     with pytest.raises(ValueError):
         channel_shard(10, 4, 4)
+
+
+class _FakeHandle:
+    """Stands in for PhaseVocoder's export_tables / import_tables on CPU."""
+
+    def __init__(self, rank):
+        g = torch.Generator().manual_seed(99 if rank == 0 else 100 + rank)
+        self.tables = torch.randint(0, 256, (4096,), dtype=torch.uint8, generator=g)
+        self.imported = 0
+
+    def export_tables(self):
+        return self.tables.clone()
+
+    def import_tables(self, blob):
+        self.tables = blob.clone()
+        self.imported += 1
+
+
+def _tables_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        h = _FakeHandle(rank)
+        same = broadcast_tables(h, src=0)
+        results[rank] = (same, h.imported, h.tables.sum().item(), int(h.tables[:8].sum()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_tables_gloo():
+    """broadcast_tables over gloo: rank 0 keeps its tables, the others import rank 0's."""
+    world, port = 3, _free_port()
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_tables_worker, args=(world, port, results), nprocs=world, join=True)
+    assert results[0][0] is True and results[0][1] == 0
+    for r in range(1, world):
+        assert results[r][0] is False and results[r][1] == 1
+        assert results[r][2:] == results[0][2:]
