@@ -314,13 +314,17 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     constexpr int N = L;  // window length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* twl = reinterpret_cast<float2*>(smem);
-    float2* tiles = twl + L;
+    float2* twsl = twl + L;                            // L+1 split twiddles (+1 pad)
+    float2* tiles = twsl + (L + 2);
+    float* winl = reinterpret_cast<float*>(tiles + 4 * G_::TILE);  // N window samples
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
+    for (int i = tid; i <= L; i += 256) twsl[i] = p.tws[i];
+    for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
     __syncthreads();
     const int run = blockIdx.x * 4 + w, c = blockIdx.y;
     if (run >= p.nruns) return;
@@ -346,15 +350,15 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
                 const long long s = base + src;
                 const float x0 = (s < p.n) ? xc[s] : 0.0f;
                 const float x1 = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
-                b0 = x0 * p.win[src];
-                b1 = x1 * p.win[src + 1];
+                b0 = x0 * winl[src];
+                b1 = x1 * winl[src + 1];
             }
             z[q] = make_float2(b0, b1);
         }
         fft_run<L, false>(z, tile, twl, tw0, lane);
         float2* srow = specc + (long long)t * p.spec_stride;
         PV_FOR_BINS(E, lane, {
-            const float2 X = real_split<L>(tile, p.tws, k);
+            const float2 X = real_split<L>(tile, twsl, k);
             const float mag = __builtin_sqrtf(X.x * X.x + X.y * X.y);
             float ph = atanf(X.y / X.x);
             if (X.x == 0.0f && X.y == 0.0f) ph = p.nan_faithful ? __builtin_nanf("") : 0.0f;
@@ -373,7 +377,7 @@ static size_t ana_lds_std(bool ekl) {
 }
 template <int L>
 static size_t ana_lds_compat() {
-    return sizeof(float2) * (L + 4 * Geo<L>::TILE);
+    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * L;
 }
 // twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with register
 // overlap-add at L <= 512 the gains live in registers and gainl is not allocated

@@ -115,6 +115,7 @@ struct PhaseMap {
     int q_pow2;
     float inv_q;
     float p_over_q;  // (p mod q) / q (RACC)
+    int multi;       // pitch ratio < 1: some bins have several sources (else at most one)
 };
 
 // LDS tables of the synthesis side (see the kernels' carve-up)
@@ -242,7 +243,8 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                 const float2 f = lds_ld(&tile[G_::pad(s >= 0 ? s : 0)]);
                 float ms = (s >= 0) ? f.x : 0.0f;
                 const float pc = (s >= 0) ? f.y : 0.0f;
-                for (int qq = 1; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
+                if (pm.multi)  // wave-uniform: ratios >= 1 never enter the loop
+                    for (int qq = 1; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
                 float sn, cs;
                 sincos_rev(pc, &sn, &cs);
                 Y[i] = make_float2(ms * cs, ms * sn);

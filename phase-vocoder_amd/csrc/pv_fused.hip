@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
     float phprev[E + 1];
     float ekr[E + 1];
     unsigned jkr[E + 1];
-    const PhaseMap pmap{p.rho * kInv2Pi, 1u, 0u, 1, 1.0f, 0.0f};
+    const PhaseMap pmap{p.rho * kInv2Pi, 1u, 0u, 1, 1.0f, 0.0f, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{twl, twsl, nullptr, nullptr, srcl};
 
     float2 acc[NS];

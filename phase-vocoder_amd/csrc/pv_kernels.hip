@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     unsigned jkr[E + 1];
     if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&ekl[k]); jkr[i] = lds_ld(&jkl[k]); })
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
-                        (float)p.p_mod * p.inv_q};
+                        (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {

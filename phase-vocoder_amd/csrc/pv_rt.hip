@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
     }
     unsigned t = p.tcount[c];
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
-                        (float)p.p_mod * p.inv_q};
+                        (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{twl, twsl, ekl, jkl, srcl};
     const float* inc = p.in + (long long)c * p.ldi;
     float* outc = p.out + (long long)c * p.ldo;

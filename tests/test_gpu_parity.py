@@ -104,8 +104,18 @@ def test_ref_compat_spectrum(cuda):
     ref = pvref.compat_analysis_frame(x, N)
     mag_ref = ref.real
     assert np.max(np.abs(spec[:2 * N, 0] - mag_ref)) <= 1e-5 * np.max(mag_ref)
+    # phase contract of atanf(Im/Re) (kernel.cu:101-109) under fp32 FFT rounding: a bin's
+    # complex value carries an absolute error of a few ulp of the frame's largest bin, so its
+    # angle is good to ~ k eps max|X| / |X_k| (conditioning), plus atanf's own ulps; the
+    # comparison is modulo pi (atan(y/x) jumps by pi where Re changes sign)
+    m = mag_ref > 0
+    d = np.abs(spec[:2 * N, 1][m].astype(np.float64) - ref.imag[m])
+    d = np.minimum(d, np.pi - d)
+    tol = 32 * np.finfo(np.float32).eps * mag_ref.max() / mag_ref[m] + 4e-7
+    assert np.all(d <= tol), f"worst excess {np.max(d / tol):.2f}x of the bound"
     big = mag_ref > 1e-3 * mag_ref.max()
-    assert np.max(np.abs(spec[:2 * N, 1][big] - ref.imag[big])) < 1e-3
+    assert np.max(np.minimum(np.abs(spec[:2 * N, 1][big] - ref.imag[big]),
+                             np.pi - np.abs(spec[:2 * N, 1][big] - ref.imag[big]))) < 2e-4
 
 
 def test_table_blob_roundtrip_and_validation(cuda):
