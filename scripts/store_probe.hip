@@ -30,7 +30,17 @@ __global__ void k_fill(unsigned* p, long long n, unsigned seed) {
     }
 }
 
-template <int S, int MAP, int BL, bool NT>
+// cache-policy bits of the row stores: 0 plain / nt (per NT), 1 sc1, 2 sc0 sc1, 3 nt sc1,
+// 4 nt sc0 sc1 (MI355X_MICROARCH.md: sc1 / sc0 sc1 stores drop the line from the XCD's L2)
+template <int POL>
+__device__ __forceinline__ void st_pol(f2* p, f2 v) {
+    if constexpr (POL == 1) asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx2 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx2 %0, %1, off nt sc0 sc1" :: "v"(p), "v"(v) : "memory");
+}
+
+template <int S, int MAP, int BL, bool NT, int POL = 0>
 __global__ __launch_bounds__(256) void k_rows(const float* __restrict__ x, f2* __restrict__ spec, int F,
                                               long long ch_samples, long long ch_spec) {
     extern __shared__ float lds_pad[];
@@ -51,12 +61,46 @@ __global__ __launch_bounds__(256) void k_rows(const float* __restrict__ x, f2* _
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const f2 v = acc + (float)i;
-            if (NT) __builtin_nontemporal_store(v, &row[lane + 64 * i]); else row[lane + 64 * i] = v;
+            if (POL) st_pol<POL>(&row[lane + 64 * i], v);
+            else if (NT) __builtin_nontemporal_store(v, &row[lane + 64 * i]); else row[lane + 64 * i] = v;
         }
         if (BL == 1) {
-            if (NT) __builtin_nontemporal_store(acc, &row[512]); else row[512] = acc;
+            if (POL) st_pol<POL>(&row[512], acc);
+            else if (NT) __builtin_nontemporal_store(acc, &row[512]); else row[512] = acc;
         } else if (BL == 2 && lane < 8) {
-            if (NT) __builtin_nontemporal_store(acc, &row[512 + lane]); else row[512 + lane] = acc;
+            if (POL) st_pol<POL>(&row[512 + lane], acc);
+            else if (NT) __builtin_nontemporal_store(acc, &row[512 + lane]); else row[512 + lane] = acc;
+        }
+    }
+}
+
+// input reads batched: every K frames a wave loads the K frames' new input (K KiB) at once,
+// then writes the K rows (tests whether the read/write interleaving costs the mix)
+template <int K>
+__global__ __launch_bounds__(256) void k_rows_batched(const float* __restrict__ x, f2* __restrict__ spec, int F,
+                                                      long long ch_samples, long long ch_spec) {
+    extern __shared__ float lds_pad[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y;
+    const float* xc = x + c * ch_samples;
+    f2* sc = spec + c * ch_spec;
+    if (lane == 64) lds_pad[0] = 0.0f;
+    f2 acc = f2((float)lane);
+    const long long r0 = (long long)(blockIdx.x * 4 + w) * F;
+    for (int u0 = 0; u0 < F; u0 += K) {
+        f2 a[K], b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            a[k] = *reinterpret_cast<const f2*>(xc + (r0 + u0 + k) * 256 + 2 * lane);
+            b[k] = *reinterpret_cast<const f2*>(xc + (r0 + u0 + k) * 256 + 128 + 2 * lane);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc += a[k] * b[k];
+            f2* row = sc + (r0 + u0 + k) * 520;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) __builtin_nontemporal_store(acc + (float)i, &row[lane + 64 * i]);
+            if (lane < 8) __builtin_nontemporal_store(acc, &row[512 + lane]);
         }
     }
 }
@@ -110,7 +154,36 @@ int main() {
     }, R), abytes)
     const long long wn = (long long)C * frames * 4104 / (256LL * 8 * 8);
     rep("write_contig_same_bytes", timeit([&] { k_write<<<wn, 256>>>((f2*)y); }, R), (double)wn * 256 * 8 * 8);
+#define ROWSP(S_, BL_, POL_, name)                                                                      \
+    rep(name, timeit([&] {                                                                               \
+        hipLaunchKernelGGL((k_rows<S_, 0, BL_, true, POL_>), grid, dim3(256), 30000, 0, (const float*)x, \
+                           (f2*)y, F, ch_samples, (long long)frames * S_);                               \
+    }, R), abytes)
+#define ROWSB(K_, name)                                                                                 \
+    rep(name, timeit([&] {                                                                               \
+        hipLaunchKernelGGL((k_rows_batched<K_>), grid, dim3(256), 30000, 0, (const float*)x, (f2*)y, F,  \
+                           ch_samples, (long long)frames * 520);                                          \
+    }, R), abytes)
     for (int pass = 0; pass < 2; ++pass) {
+        ROWS(520, 0, 2, true, 30000, "s520_bl2_nt");
+        ROWSB(1, "batched_K1");
+        ROWSB(2, "batched_K2");
+        ROWSB(4, "batched_K4");
+        ROWSB(8, "batched_K8");
+        ROWSB(16, "batched_K16");
+    }
+    for (int pass = 0; pass < 0; ++pass) {
+        ROWS(520, 0, 1, true, 30000, "s520_bl1_nt (product)");
+        ROWSP(520, 1, 1, "s520_bl1_sc1");
+        ROWSP(520, 1, 2, "s520_bl1_sc0sc1");
+        ROWSP(520, 1, 3, "s520_bl1_ntsc1");
+        ROWSP(520, 1, 4, "s520_bl1_ntsc0sc1");
+        ROWS(520, 0, 2, true, 30000, "s520_bl2_nt");
+        ROWSP(520, 2, 1, "s520_bl2_sc1");
+        ROWSP(520, 2, 2, "s520_bl2_sc0sc1");
+        ROWSP(520, 2, 3, "s520_bl2_ntsc1");
+    }
+    for (int pass = 0; pass < 0; ++pass) {
         ROWS(520, 0, 1, true, 30000, "s520_map0_bl1_lds30k (product)");
         ROWS(520, 0, 1, true, 0, "s520_map0_bl1_lds0");
         ROWS(520, 0, 2, true, 30000, "s520_map0_bl2_lds30k");
