@@ -16,7 +16,8 @@
 #include "pv_kernels.h"
 
 #ifndef PV_SYN_GREG
-#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512)
+#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512); PV_SYN_1BUF
+                       // needs them in LDS (0) to fit 4 waves/SIMD
 #endif
 
 namespace pv {
@@ -132,7 +133,11 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 #define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
 #endif
 #ifndef PV_SYN_1BUF
-#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame
+#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame.  With
+                       // PV_SYN_GREG=0 PV_SYN_WAVES512=4: 118-120 VGPRs, 4 waves/SIMD instead of
+                       // 3; config 3 synthesis -5 % but the analysis +2 % (the denser
+                       // synthesis lowers the chip's clock for both), step +1.1 %
+                       // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
 #endif
 #ifndef PV_SYN_KREG
 #define PV_SYN_KREG 0  // measured: no gain over the LDS reads
@@ -287,15 +292,6 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
         // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
         // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
         // alternate (F is even), so no register copies carry a row across trips.
-        auto step = [&](int u, const f2v (&row)[E + 1]) {
-            float2 sv[E + 1];
-#pragma unroll
-            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
-            float2 z[E];
-            synth(u, t0 + u, sv, z);
-            ola_regs(z);
-            flush_regs(u, std::true_type{});  // exactly D stores
-        };
         auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
 #if PV_SYN_1BUF
         // one row buffer: row u+1 is loaded into it once frame u's phase stage has
@@ -315,6 +311,15 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
             vm_wait<D>(row);
         }
 #else
+        auto step = [&](int u, const f2v (&row)[E + 1]) {
+            float2 sv[E + 1];
+#pragma unroll
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
+            float2 z[E];
+            synth(u, t0 + u, sv, z);
+            ola_regs(z);
+            flush_regs(u, std::true_type{});  // exactly D stores
+        };
         f2v ra[E + 1], rb[E + 1];
         gload_row<E>(ra, rowp(0) + lane, rowp(0) + L);
         vm_wait<0>(ra);
