@@ -230,7 +230,10 @@ def main():
                  "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
                  "carry": 0, "runsum": 8 * B, "seam": 0,
                  # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
-                 "fused": 4 * hop_a + 8 * B + 4 * hop_s}
+                 "fused": 4 * hop_a + 8 * B + 4 * hop_s,
+                 # q = 2^e single launch chained over run groups (pv_chain.hip): the spectrum is
+                 # written once (an output) and re-read from L2 / MALL, not counted twice
+                 "chain": 4 * hop_a + 8 * B + 4 * hop_s}
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     avg_ms = ms_tot / max(launches, 1)

@@ -161,12 +161,12 @@ __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
 #endif
 // one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and bin L (the
 // same address on every lane) from rowL
-template <int E>
+template <int E, bool NT = (bool)PV_NT_ROWS>
 __device__ __forceinline__ void gload_row(f2v (&v)[E + 1], const float2* rowlane, const float2* rowL) {
     f2v (&head)[E] = *reinterpret_cast<f2v(*)[E]>(&v[0]);
-    // rows are read exactly once: PV_NT_ROWS streams them past the caches
-    gload_pairs<E, (bool)PV_NT_ROWS>(head, reinterpret_cast<const float*>(rowlane));
-    if constexpr ((bool)PV_NT_ROWS)
+    // rows are read exactly once: NT (PV_NT_ROWS) streams them past the caches
+    gload_pairs<E, NT>(head, reinterpret_cast<const float*>(rowlane));
+    if constexpr (NT)
         asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v[E]) : "v"(rowL) : "memory");
     else
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");

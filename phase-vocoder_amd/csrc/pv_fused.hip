@@ -19,33 +19,15 @@
 // Geometry as k_synthesis: a wave = a run of F frames of one channel, 4 runs per workgroup,
 // the intra-workgroup seams closed after one barrier, the inter-workgroup seams by the
 // second of the two workgroups to finish (no k_seam launch).
-#include "pv_frame.hpp"
-#include "pv_kernels.h"
+#include "pv_syn_run.hpp"
 
 namespace pv {
 
-// Inter-workgroup hand-off without fences (MI355X_MICROARCH.md, "Valid forms": write-through
-// `sc1` stores of every handed-off byte, the storing wave's vmcnt(0) before its counter add,
-// `sc1` loads of them after the add has returned): an agent-scope release/acquire pair
-// would write back / invalidate whole caches (buffer_wbl2 / buffer_inv) per workgroup.
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_sc1(float* p, f2v v) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-    float v;
-    asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-// counter add after every store of the wave has left (relaxed: the sc1 stores need no fence)
-__device__ __forceinline__ int arrive(int* flag, int lane) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __shfl(old, 0);
-}
+// Inter-workgroup hand-offs: st_sc1 / ld_sc1 / arrive / close_seams_inline (pv_syn_run.hpp),
+// write-through `sc1` stores of every handed-off byte, the storing wave's vmcnt(0) before its
+// counter add, `sc1` loads of them after the add has returned (MI355X_MICROARCH.md "Valid
+// forms"): an agent-scope release/acquire pair would write back / invalidate whole caches
+// (buffer_wbl2 / buffer_inv) per workgroup.
 
 template <int L>
 struct FuGeo {
@@ -210,67 +192,8 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
     }
-    // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
-    __syncthreads();
-    float* rings = reinterpret_cast<float*>(tiles);
-    float* ring = rings + w * N;
-    {
-        float2* r2 = reinterpret_cast<float2*>(ring);
-#pragma unroll
-        for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
-    }
-    __syncthreads();
-    // seams: run w's tail overlaps run w+1's head
-    if (w > 0) {
-        const float* prev = rings + (w - 1) * N;
-        for (int j = lane; j < TL; j += 64) {
-            const long long gp = obase + j;
-            if (gp < p.out_len) outc[gp] += prev[j];
-        }
-    }
-    // Inter-workgroup seam b (workgroup b-1's last tail overlaps workgroup b's head, which
-    // wave 0 of workgroup b stored as if final): closed in this launch by whichever of the
-    // two sides arrives second.  Each side publishes its part write-through (the tail to
-    // `tails`, the head to `out`), waits for its stores, then adds 1 to the seam's counter;
-    // the side whose add returns 1 reads the other part (sc1 loads), writes head + tail and
-    // resets the counter for the next launch.  Nobody waits for anybody, so there is no
-    // dispatch-order assumption; head + tail is the same float whoever adds it.
-    const int nwg = (p.nruns + 3) / 4;
-    if (w == 3) {
-        const bool last = (blockIdx.x + 1 >= nwg);
-        float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len;
-        const long long nbase = obase + (long long)p.F * hs;  // workgroup b+1's first position
-        for (int j = lane; j < TL; j += 64) {
-            const float v = ring[j];
-            if (last) {
-                const long long gp = nbase + j;
-                if (gp < p.out_len) outc[gp] = v;
-            } else {
-                st_sc1(tdst + j, v);
-            }
-        }
-        if (!last) {
-            int* flag = p.seam_flags + (long long)c * nwg + blockIdx.x;
-            if (arrive(flag, lane) == 1) {  // workgroup b+1's head is in out
-                for (int j = lane; j < TL; j += 64) {
-                    const long long gp = nbase + j;
-                    if (gp < p.out_len) outc[gp] = ld_sc1(outc + gp) + ring[j];
-                }
-                if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-    if (w == 0 && blockIdx.x > 0) {
-        int* flag = p.seam_flags + (long long)c * nwg + (blockIdx.x - 1);
-        if (arrive(flag, lane) == 1) {  // workgroup b-1's tail is in tails
-            const float* tsrc = p.tails + ((long long)c * nwg + (blockIdx.x - 1)) * p.tail_len;
-            for (int j = lane; j < TL; j += 64) {
-                const long long gp = obase + j;
-                if (gp < p.out_len) outc[gp] = ld_sc1(outc + gp) + ld_sc1(tsrc + j);
-            }
-            if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    close_seams_inline<L, NS, D>(acc, tiles, w, lane, c, blockIdx.x, (p.nruns + 3) / 4, obase, p.F, hs, outc,
+                                 p.out_len, p.tails, p.tail_len, p.seam_flags);
 }
 
 bool fused_supported(int L, int hs) {

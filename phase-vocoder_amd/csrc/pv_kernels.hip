@@ -12,13 +12,7 @@
 // Geometry: one frame per wavefront, and each wave owns a RUN of F consecutive frames of
 // one channel which it walks in order (the unwrap state stays in registers, the
 // overlap-add in a per-wave LDS ring).  A workgroup = 4 waves = 4 consecutive runs.
-#include "pv_frame.hpp"
-#include "pv_kernels.h"
-
-#ifndef PV_SYN_GREG
-#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512); PV_SYN_1BUF
-                       // needs them in LDS (0) to fit 4 waves/SIMD
-#endif
+#include "pv_syn_run.hpp"
 
 namespace pv {
 
@@ -126,34 +120,21 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
-#ifndef PV_NT_OUT
-#define PV_NT_OUT 1  // non-temporal output stores in the synthesis (-0.5 %)
-#endif
-#ifndef PV_REV_ACC
-#define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
-#endif
-#ifndef PV_SYN_1BUF
-#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame.  With
-                       // PV_SYN_GREG=0 PV_SYN_WAVES512=4: 118-120 VGPRs, 4 waves/SIMD instead of
-                       // 3; config 3 synthesis -5 % but the analysis +2 % (the denser
-                       // synthesis lowers the chip's clock for both), step +1.1 %
-                       // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
-#endif
-#ifndef PV_SYN_KREG
-#define PV_SYN_KREG 0  // measured: no gain over the LDS reads
-#endif
 #ifndef PV_SYN_WAVES512
 #define PV_SYN_WAVES512 3  // waves per SIMD the L = 512 synthesis is compiled for
 #endif
+#ifndef PV_SYN_WAVES1024
+#define PV_SYN_WAVES1024 1  // waves per SIMD the L = 1024 synthesis is compiled for
+#endif
 template <int L, int MODE, int DT, bool QPOW2 = false>
-__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 : 1) void k_synthesis(SynParams p) {
+__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 : (L == 1024) ? PV_SYN_WAVES1024 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int SPW = N / 64;  // samples per lane per frame
     constexpr int B = L + 1;
-    constexpr bool GREG = PV_SYN_GREG && ROLA && L <= 512;  // ROLA gains in registers (else LDS)
+    constexpr bool GREG = SynTraits<L, MODE, DT, QPOW2>::GREG;  // ROLA gains in registers (else LDS)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* twl = reinterpret_cast<float2*>(smem);                     // L
     float2* twsl = twl + L;                                            // L (+2 pad)
@@ -168,7 +149,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     int* srcl = reinterpret_cast<int*>(jkl + (B + 3));                 // 2 x B (pitch)
     const int hs = p.hs;
     const int TL = N - hs;
-    constexpr bool RACC = QPOW2 && MODE != 1 && PV_REV_ACC;  // host: QPOW2 only for q <= 4096
+    constexpr bool RACC = SynTraits<L, MODE, DT, QPOW2>::RACC;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
@@ -196,8 +177,6 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     const int run = blockIdx.x * 4 + w;
     const int t0 = run * p.F;
     const int nfr = max(0, min(p.F, p.frames - t0));  // real frames of this wave's run
-    float2* tile = tiles + w * G_::TILE;
-    const float2* specc = p.spec + (long long)c * p.ld_spec;
     float* outc = p.out + (long long)c * p.ldo;
     const long long obase = (long long)t0 * hs;
 
@@ -217,174 +196,10 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
             PV_FOR_BINS(E, lane, { M[i] = cr ? cr[k] : 0; phprev[i] = 0.0f; })
         }
     }
-
-    // ROLA state: acc[c] = run positions u*hs + 128 c + 2 lane + {0,1}; gains likewise
-    constexpr int NS = ROLA ? E : 1;
-    constexpr int D = ROLA ? DT : 1;  // slots completed per frame (ROLA)
-    float2 acc[NS], gn[GREG ? NS : 1];
-    if (ROLA) {
-        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            acc[s] = make_float2(0.0f, 0.0f);
-            if constexpr (GREG) gn[s] = g2[64 * s + lane];
-        }
-    }
-
-    // unwrap constants of the lane's bins in registers for the whole run (ROLA kernels
-    // have VGPRs to spare below their LDS-bound occupancy)
-    constexpr bool KREG = ROLA && MODE == 0 && PV_SYN_KREG;  // pitch (MODE 2) would spill
-    float ekr[E + 1];
-    unsigned jkr[E + 1];
-    if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&ekl[k]); jkr[i] = lds_ld(&jkl[k]); })
-    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
-                        (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
-    const SynLds stb{twl, twsl, ekl, jkl, srcl};
-    const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
-    auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
-        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
-    };
-    [[maybe_unused]] auto synth_h = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hook) {
-        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook);
-    };
-    // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
-    // moves raw slot cr to OLA slot cr + E/2 (mod E)
-    auto ola_regs = [&](const float2 (&z)[E]) {
-#pragma unroll
-        for (int idx = 0; idx < E; ++idx) {
-            const int cr = last_slot<L>(idx);
-            const int cs = (MODE == 1) ? ((cr + E / 2) & (E - 1)) : cr;
-            const float2 g = GREG ? gn[GREG ? cs : 0]
-                                  : lds_ld(reinterpret_cast<const float2*>(gainl) + 64 * cs + lane);
-            acc[cs].x = __builtin_fmaf(z[idx].x, g.x, acc[cs].x);
-            acc[cs].y = __builtin_fmaf(z[idx].y, g.y, acc[cs].y);
-        }
-    };
-    // ROLA flush of frame u: positions [u*hs, (u+1)*hs) = slots 0..D-1 are final
-    auto flush_regs = [&](int u, auto fast_tag) {
-        constexpr bool FAST = decltype(fast_tag)::value;
-        const long long pb = obase + (long long)u * hs + 2 * lane;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const long long gp = pb + 128 * d;
-            if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
-#if PV_NT_OUT
-                __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
-#else
-                *reinterpret_cast<float2*>(outc + gp) = acc[d];
-#endif
-            } else {
-                if (gp < p.out_len) outc[gp] = acc[d].x;
-                if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
-    };
-
-    // the self-tracked prefetch needs registers that are never spilled or copied while the
-    // loads are in flight: only at L <= 512, where the kernels fit without spills
-    constexpr bool FASTOK = ROLA && L <= 512;
-    const bool fast = FASTOK && nfr == p.F && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
-    if (FASTOK && fast) {
-        // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
-        // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
-        // alternate (F is even), so no register copies carry a row across trips.
-        auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
-#if PV_SYN_1BUF
-        // one row buffer: row u+1 is loaded into it once frame u's phase stage has
-        // consumed it (synth_frame hook), then the pre-step, FFT and overlap-add run
-        // while it is in flight: 18 VGPRs fewer than two buffers
-        f2v row[E + 1];
-        gload_row<E>(row, rowp(0) + lane, rowp(0) + L);
-        vm_wait<0>(row);
-        for (int u = 0; u < p.F; ++u) {
-            float2 sv[E + 1];
-#pragma unroll
-            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
-            float2 z[E];
-            synth_h(u, t0 + u, sv, z, [&] { gload_row<E>(row, rowp(u + 1) + lane, rowp(u + 1) + L); });
-            ola_regs(z);
-            flush_regs(u, std::true_type{});  // exactly D stores
-            vm_wait<D>(row);
-        }
-#else
-        auto step = [&](int u, const f2v (&row)[E + 1]) {
-            float2 sv[E + 1];
-#pragma unroll
-            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
-            float2 z[E];
-            synth(u, t0 + u, sv, z);
-            ola_regs(z);
-            flush_regs(u, std::true_type{});  // exactly D stores
-        };
-        f2v ra[E + 1], rb[E + 1];
-        gload_row<E>(ra, rowp(0) + lane, rowp(0) + L);
-        vm_wait<0>(ra);
-        for (int u = 0; u < p.F; u += 2) {
-            gload_row<E>(rb, rowp(u + 1) + lane, rowp(u + 1) + L);
-            step(u, ra);
-            vm_wait<D>(rb);
-            gload_row<E>(ra, rowp(u + 2) + lane, rowp(u + 2) + L);
-            step(u + 1, rb);
-            vm_wait<D>(ra);
-        }
-#endif
-    } else {
-        float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
-        if (nfr > 0) {
-            const float2* srow = specc + (long long)t0 * p.spec_stride;
-            PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-        }
-        for (int u = 0; u < p.F; ++u) {
-            const int t = t0 + u;
-            if (u < nfr) {
-                float2 cur[E + 1];
-#pragma unroll
-                for (int i = 0; i <= E; ++i) cur[i] = sv[i];
-                if (u + 1 < nfr) {
-                    const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
-                    PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-                }
-                float2 z[E];
-                synth(u, t, cur, z);
-                if constexpr (ROLA) {
-                    ola_regs(z);
-                } else {
-                    // overlap-add the frame into the ring (lane-distinct positions)
-                    // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
-                    // 2 pad(nn >> 1) + (nn & 1) = per-lane base + compile-time offset
-                    constexpr int ROT = (MODE == 1) ? N / 2 : 0;
-                    const float* ty = reinterpret_cast<const float*>(tile) + 2 * G_::pad(lane >> 1) + (lane & 1);
-                    const int rbase = u * hs + lane;
-#pragma unroll
-                    for (int i = 0; i < SPW; ++i) {
-                        const int n = lane + 64 * i;
-                        const int cc = ((64 * i + ROT) & (N - 1)) >> 1;
-                        const float yv = ty[2 * G_::padc(cc)];
-                        const int pos = (rbase + 64 * i) & (N - 1);
-                        ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
-                    }
-                    wave_lds_sync();
-                }
-            }
-            if constexpr (ROLA) {
-                flush_regs(u, std::false_type{});
-            } else {
-                // positions [u*hs, (u+1)*hs) are final for this run
-                for (int j = lane; j < hs; j += 64) {
-                    const int pl = u * hs + j;
-                    const int slot = pl & (N - 1);
-                    const float v = ring[slot];
-                    ring[slot] = 0.0f;
-                    if (obase + pl < p.out_len) outc[obase + pl] = v;
-                }
-                wave_lds_sync();
-            }
-        }
-    }
+    constexpr int NS = SynTraits<L, MODE, DT, QPOW2>::NS, D = SynTraits<L, MODE, DT, QPOW2>::D;
+    float2 acc[NS];
+    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, false>(
+        p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, false, M, phprev, acc);
     if constexpr (ROLA) {
         // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
         __syncthreads();

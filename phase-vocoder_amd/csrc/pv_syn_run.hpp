@@ -1,0 +1,354 @@
+// pv_syn_run.hpp — one wave's synthesis run (phase propagation -> polar->rect -> inverse
+// real FFT -> window -> overlap-add -> final samples to `out`), shared by the split path's
+// K3 (k_synthesis, pv_kernels.hip) and the single-launch chained path (k_chain,
+// pv_chain.hip).  Geometry and overlap-add: pv_kernels.hip, K3.
+#pragma once
+#include "pv_frame.hpp"
+#include "pv_kernels.h"
+
+#ifndef PV_SYN_GREG
+#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512); PV_SYN_1BUF
+                       // needs them in LDS (0) to fit 4 waves/SIMD
+#endif
+#ifndef PV_NT_OUT
+#define PV_NT_OUT 1  // non-temporal output stores in the synthesis (-0.5 %)
+#endif
+#ifndef PV_REV_ACC
+#define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
+#endif
+#ifndef PV_SYN_1BUF
+#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame.  With
+                       // PV_SYN_GREG=0 PV_SYN_WAVES512=4: 118-120 VGPRs, 4 waves/SIMD instead of
+                       // 3; config 3 synthesis -5 % but the analysis +2 % (the denser
+                       // synthesis lowers the chip's clock for both), step +1.1 %
+                       // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
+#endif
+#ifndef PV_SYN_KREG
+#define PV_SYN_KREG 0  // measured: no gain over the LDS reads
+#endif
+
+namespace pv {
+
+// sc1 (write-through) stores / loads of the inter-workgroup hand-offs (pv_fused.hip,
+// pv_chain.hip; MI355X_MICROARCH.md "Valid forms")
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(float* p, f2v v) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+// counter add after every store of the wave has left (relaxed: the sc1 stores need no fence)
+__device__ __forceinline__ int arrive(int* flag, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __shfl(old, 0);
+}
+
+// After a register overlap-add run (wave w of a workgroup of 4 consecutive runs, workgroup
+// index wg of nwg along the channel): the run's tail -> ring (LDS, over the tiles), the three
+// intra-workgroup seams from the neighbours' tails, and the inter-workgroup seams in the
+// same launch.  Seam b (workgroup b-1's last tail overlaps workgroup b's head, which wave 0
+// of workgroup b stored write-through as if final) is closed by whichever side arrives
+// second: each side publishes its part write-through (the tail to `tails`, the head to
+// `out`), waits for its stores and adds 1 to the seam's counter; the side whose add returns
+// 1 reads the other part (sc1 loads), writes head + tail and resets the counter for the next
+// launch.  Nobody waits for anybody, so there is no dispatch-order assumption; head + tail
+// is the same float whoever adds it.  Every wave of the workgroup must call this.
+template <int L, int NS, int D>
+__device__ __forceinline__ void close_seams_inline(const float2 (&acc)[NS], float2* tiles, int w, int lane, int c,
+                                                   int wg, int nwg, long long obase, int F, int hs, float* outc,
+                                                   long long out_len, float* tails, int tail_len, int* seam_flags) {
+    constexpr int N = 2 * L;
+    const int TL = N - hs;
+    __syncthreads();
+    float* rings = reinterpret_cast<float*>(tiles);
+    float* ring = rings + w * N;
+    {
+        float2* r2 = reinterpret_cast<float2*>(ring);
+#pragma unroll
+        for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
+    }
+    __syncthreads();
+    // seams: run w's tail overlaps run w+1's head
+    if (w > 0) {
+        const float* prev = rings + (w - 1) * N;
+        for (int j = lane; j < TL; j += 64) {
+            const long long gp = obase + j;
+            if (gp < out_len) outc[gp] += prev[j];
+        }
+    }
+    if (w == 3) {
+        const bool last = (wg + 1 >= nwg);
+        float* tdst = tails + ((long long)c * nwg + wg) * tail_len;
+        const long long nbase = obase + (long long)F * hs;  // workgroup wg+1's first position
+        for (int j = lane; j < TL; j += 64) {
+            const float v = ring[j];
+            if (last) {
+                const long long gp = nbase + j;
+                if (gp < out_len) outc[gp] = v;
+            } else {
+                st_sc1(tdst + j, v);
+            }
+        }
+        if (!last) {
+            int* flag = seam_flags + (long long)c * nwg + wg;
+            if (arrive(flag, lane) == 1) {  // workgroup wg+1's head is in out
+                for (int j = lane; j < TL; j += 64) {
+                    const long long gp = nbase + j;
+                    if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ring[j];
+                }
+                if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (w == 0 && wg > 0) {
+        int* flag = seam_flags + (long long)c * nwg + (wg - 1);
+        if (arrive(flag, lane) == 1) {  // workgroup wg-1's tail is in tails
+            const float* tsrc = tails + ((long long)c * nwg + (wg - 1)) * tail_len;
+            for (int j = lane; j < TL; j += 64) {
+                const long long gp = obase + j;
+                if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ld_sc1(tsrc + j);
+            }
+            if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// LDS carve-up pointers of the synthesis (the kernels lay them out differently)
+struct SynCarve {
+    const float2* twl;   // stage-major twiddles, L-point
+    const float2* twsl;  // e^{-2 pi i k/N}, k <= L
+    float2* tiles;       // 4 x TILE
+    float* rings;        // DT = 0: 4 x N overlap-add rings (live through the loop)
+    const float* gainl;  // N gains (unless GREG)
+    const float* ekl;    // e_k
+    const unsigned* jkl; // (p j_k) mod q, or its float / q (RACC)
+    const int* srcl;     // pitch map {first, count}
+};
+
+template <int L, int MODE, int DT, bool QPOW2>
+struct SynTraits {
+    static constexpr bool ROLA = DT > 0;
+    static constexpr int E = Geo<L>::E;
+    static constexpr int NS = ROLA ? E : 1;  // register overlap-add slots
+    static constexpr int D = ROLA ? DT : 1;  // slots completed per frame (ROLA)
+    static constexpr bool GREG = PV_SYN_GREG && ROLA && L <= 512;
+    static constexpr bool RACC = QPOW2 && MODE != 1 && PV_REV_ACC;  // host: QPOW2 only for q <= 4096
+};
+
+// The frame loop of one wave's run: frames t0 .. t0 + F - 1 of channel c (frames >= nfr are
+// zero), unwrap state M / phprev initialised by the caller (M = the carry at t0, in the RACC
+// form when RACC).  On return acc holds the run's overlap tail (ROLA; slots D..NS-1) or
+// the ring does (DT = 0).
+// NTROW: spectrum rows loaded non-temporally.  HEADSC1: the positions < N - hs of a run
+// whose workgroup has a predecessor (head) are stored write-through (sc1) for an in-kernel
+// seam hand-off; `head` says whether this wave's run is such a head.
+template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool HEADSC1>
+__device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, const float2 (&tw0)[Geo<L>::E],
+                                        int lane, int w, int c, int t0, int nfr, bool head,
+                                        int (&M)[Geo<L>::E + 1], float (&phprev)[Geo<L>::E + 1],
+                                        float2 (&acc)[SynTraits<L, MODE, DT, QPOW2>::NS]) {
+    using G_ = Geo<L>;
+    using T_ = SynTraits<L, MODE, DT, QPOW2>;
+    constexpr bool ROLA = T_::ROLA;
+    constexpr int E = G_::E;
+    constexpr int N = 2 * L;
+    constexpr int SPW = N / 64;  // samples per lane per frame
+    constexpr int NS = T_::NS;
+    constexpr int D = T_::D;
+    constexpr bool GREG = T_::GREG;
+    constexpr bool RACC = T_::RACC;
+    const int hs = p.hs;
+    const int TL = N - hs;
+    (void)TL; (void)head;
+    float2* tile = sc.tiles + w * G_::TILE;
+    float* ring = sc.rings + w * N;
+    const float* gainl = sc.gainl;
+    (void)gainl; (void)ring;
+    const float2* specc = p.spec + (long long)c * p.ld_spec;
+    float* outc = p.out + (long long)c * p.ldo;
+    const long long obase = (long long)t0 * hs;
+
+    float2 gn[GREG ? NS : 1];
+    if (ROLA) {
+        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            acc[s] = make_float2(0.0f, 0.0f);
+            if constexpr (GREG) gn[s] = g2[64 * s + lane];
+        }
+    }
+
+    // unwrap constants of the lane's bins in registers for the whole run (ROLA kernels
+    // have VGPRs to spare below their LDS-bound occupancy)
+    constexpr bool KREG = ROLA && MODE == 0 && PV_SYN_KREG;  // pitch (MODE 2) would spill
+    float ekr[E + 1];
+    unsigned jkr[E + 1];
+    if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&sc.ekl[k]); jkr[i] = lds_ld(&sc.jkl[k]); })
+    const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
+                        (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
+    const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};
+    const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
+    auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
+        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
+    };
+    [[maybe_unused]] auto synth_h = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hook) {
+        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook);
+    };
+    // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
+    // moves raw slot cr to OLA slot cr + E/2 (mod E)
+    auto ola_regs = [&](const float2 (&z)[E]) {
+#pragma unroll
+        for (int idx = 0; idx < E; ++idx) {
+            const int cr = last_slot<L>(idx);
+            const int cs = (MODE == 1) ? ((cr + E / 2) & (E - 1)) : cr;
+            const float2 g = GREG ? gn[GREG ? cs : 0]
+                                  : lds_ld(reinterpret_cast<const float2*>(gainl) + 64 * cs + lane);
+            acc[cs].x = __builtin_fmaf(z[idx].x, g.x, acc[cs].x);
+            acc[cs].y = __builtin_fmaf(z[idx].y, g.y, acc[cs].y);
+        }
+    };
+    // ROLA flush of frame u: positions [u*hs, (u+1)*hs) = slots 0..D-1 are final
+    auto flush_regs = [&](int u, auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        const long long pb = obase + (long long)u * hs + 2 * lane;
+        // head positions of a chained workgroup go out write-through (wave-uniform)
+        const bool hd = HEADSC1 && head && (u * hs < TL);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const long long gp = pb + 128 * d;
+            if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
+                if (HEADSC1 && hd) {
+                    st_sc1(outc + gp, f2v{acc[d].x, acc[d].y});
+                } else {
+#if PV_NT_OUT
+                    __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
+#else
+                    *reinterpret_cast<float2*>(outc + gp) = acc[d];
+#endif
+                }
+            } else if (HEADSC1 && hd) {
+                if (gp < p.out_len) st_sc1(outc + gp, acc[d].x);
+                if (gp + 1 < p.out_len) st_sc1(outc + gp + 1, acc[d].y);
+            } else {
+                if (gp < p.out_len) outc[gp] = acc[d].x;
+                if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
+    };
+
+    // the self-tracked prefetch needs registers that are never spilled or copied while the
+    // loads are in flight: only at L <= 512, where the kernels fit without spills
+    constexpr bool FASTOK = ROLA && L <= 512;
+    const bool fast = FASTOK && nfr == p.F && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
+    if (FASTOK && fast) {
+        // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
+        // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
+        // alternate (F is even), so no register copies carry a row across trips.
+        auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
+#if PV_SYN_1BUF
+        // one row buffer: row u+1 is loaded into it once frame u's phase stage has
+        // consumed it (synth_frame hook), then the pre-step, FFT and overlap-add run
+        // while it is in flight: 18 VGPRs fewer than two buffers
+        f2v row[E + 1];
+        gload_row<E, NTROW>(row, rowp(0) + lane, rowp(0) + L);
+        vm_wait<0>(row);
+        for (int u = 0; u < p.F; ++u) {
+            float2 sv[E + 1];
+#pragma unroll
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
+            float2 z[E];
+            synth_h(u, t0 + u, sv, z, [&] { gload_row<E, NTROW>(row, rowp(u + 1) + lane, rowp(u + 1) + L); });
+            ola_regs(z);
+            flush_regs(u, std::true_type{});  // exactly D stores
+            vm_wait<D>(row);
+        }
+#else
+        auto step = [&](int u, const f2v (&row)[E + 1]) {
+            float2 sv[E + 1];
+#pragma unroll
+            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
+            float2 z[E];
+            synth(u, t0 + u, sv, z);
+            ola_regs(z);
+            flush_regs(u, std::true_type{});  // exactly D stores
+        };
+        f2v ra[E + 1], rb[E + 1];
+        gload_row<E, NTROW>(ra, rowp(0) + lane, rowp(0) + L);
+        vm_wait<0>(ra);
+        for (int u = 0; u < p.F; u += 2) {
+            gload_row<E, NTROW>(rb, rowp(u + 1) + lane, rowp(u + 1) + L);
+            step(u, ra);
+            vm_wait<D>(rb);
+            gload_row<E, NTROW>(ra, rowp(u + 2) + lane, rowp(u + 2) + L);
+            step(u + 1, rb);
+            vm_wait<D>(ra);
+        }
+#endif
+    } else {
+        float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
+        if (nfr > 0) {
+            const float2* srow = specc + (long long)t0 * p.spec_stride;
+            PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
+        }
+        for (int u = 0; u < p.F; ++u) {
+            const int t = t0 + u;
+            if (u < nfr) {
+                float2 cur[E + 1];
+#pragma unroll
+                for (int i = 0; i <= E; ++i) cur[i] = sv[i];
+                if (u + 1 < nfr) {
+                    const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
+                    PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
+                }
+                float2 z[E];
+                synth(u, t, cur, z);
+                if constexpr (ROLA) {
+                    ola_regs(z);
+                } else {
+                    // overlap-add the frame into the ring (lane-distinct positions)
+                    // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
+                    // 2 pad(nn >> 1) + (nn & 1) = per-lane base + compile-time offset
+                    constexpr int ROT = (MODE == 1) ? N / 2 : 0;
+                    const float* ty = reinterpret_cast<const float*>(tile) + 2 * G_::pad(lane >> 1) + (lane & 1);
+                    const int rbase = u * hs + lane;
+#pragma unroll
+                    for (int i = 0; i < SPW; ++i) {
+                        const int n = lane + 64 * i;
+                        const int cc = ((64 * i + ROT) & (N - 1)) >> 1;
+                        const float yv = ty[2 * G_::padc(cc)];
+                        const int pos = (rbase + 64 * i) & (N - 1);
+                        ring[pos] = __builtin_fmaf(yv, gainl[n], ring[pos]);
+                    }
+                    wave_lds_sync();
+                }
+            }
+            if constexpr (ROLA) {
+                flush_regs(u, std::false_type{});
+            } else {
+                // positions [u*hs, (u+1)*hs) are final for this run
+                for (int j = lane; j < hs; j += 64) {
+                    const int pl = u * hs + j;
+                    const int slot = pl & (N - 1);
+                    const float v = ring[slot];
+                    ring[slot] = 0.0f;
+                    if (obase + pl < p.out_len) outc[obase + pl] = v;
+                }
+                wave_lds_sync();
+            }
+        }
+    }
+}
+
+}  // namespace pv

@@ -34,7 +34,8 @@ class pv_info(ctypes.Structure):
     _fields_ = [("n_samps", ctypes.c_int), ("hop", ctypes.c_int), ("out_hop", ctypes.c_int),
                 ("spec_bins", ctypes.c_int), ("spec_stride", ctypes.c_int),
                 ("frames_per_run", ctypes.c_int), ("mode", ctypes.c_int), ("effect", ctypes.c_int),
-                ("scale", ctypes.c_float)]
+                ("scale", ctypes.c_float), ("single_launch", ctypes.c_int),
+                ("single_launch_frames", ctypes.c_int)]
 
 
 _lib = None
@@ -83,6 +84,9 @@ def lib():
     L.pv_set_window.restype = i
     L.pv_test_overlap_add.argtypes = [vp, vp, vp, vp, i, i, vp]
     L.pv_test_overlap_add.restype = i
+    if hasattr(L, "pv_check_device"):  # (A/B builds of older revisions lack it)
+        L.pv_check_device.argtypes = [vp]
+        L.pv_check_device.restype = i
     L.pv_profile_enable.argtypes = [vp, i]
     L.pv_profile_enable.restype = i
     L.pv_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),

@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.pv_abi_version() == 2
+    assert L.pv_abi_version() == 3
     assert L.pv_status_string(0) == b"PV_OK"
     assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
 
