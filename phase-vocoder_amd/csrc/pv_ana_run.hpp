@@ -32,6 +32,12 @@
 #define PV_ANA_CH 3  // analysis: bins per batch of LDS reads + atan2 chains
 #endif
 
+#ifdef PV_ABL_NOFFT
+#define PV_ABL_NOFFT_ON 1
+#else
+#define PV_ABL_NOFFT_ON 0
+#endif
+
 namespace pv {
 
 // LDS tables the analysis reads (the kernels' carve-ups differ)
@@ -59,6 +65,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
+    constexpr bool SPLIT_BP = PV_SPLIT_BP && !PV_ABL_NOFFT_ON;
     const int BP = p.bins_pad;
     const float2* twl = lt.twl;
     const float2* twsl = lt.twsl;
@@ -88,14 +95,16 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         pass_store<L, Geo<L>::NPASS - 1>(z, tile, lane);
         wave_lds_sync();
 #else
-        fft_run<L, false>(z, tile, twl, tw0, lane);
+        // SPLIT_BP: the last pass's registers feed the split directly (no final image)
+        fft_run<L, false, !SPLIT_BP>(z, tile, twl, tw0, lane);
 #endif
         // bins in chunks of CH (bounded live registers), all reads of a chunk batched
         constexpr int CH = PV_ANA_CH;
-#pragma unroll
-        for (int i0 = 0; i0 <= E; i0 += CH) {
+        static_for<0, (E + CH) / CH>([&](auto ic) {
+            constexpr int i0 = decltype(ic)::value * CH;
             float2 X[CH];
-            split_chunk<L, CH, PV_SPLIT2X>(tile, twsl, lane, i0, X);
+            if constexpr (SPLIT_BP) split_chunk_bp<L, CH, PV_SPLIT2X, i0>(z, twsl, lane, X);
+            else split_chunk<L, CH, PV_SPLIT2X>(tile, twsl, lane, i0, X);
 #pragma unroll
             for (int c2 = 0; c2 < CH; ++c2) {
                 const int i = i0 + c2;
@@ -147,7 +156,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                 }
                 phprev[i] = ph;
             }
-        }
+        });
         wave_lds_sync();  // tile reads done before the next frame's pass_store
     };
     auto load_fast = [&](int u, float2 (&xr)[E]) {

@@ -22,6 +22,20 @@ constexpr int bitrevc(int v, int bits) {
 }
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1 (register-array
+// indices that must fold to constants, where #pragma unroll may give up on a large body)
+template <int I>
+struct IC {
+    static constexpr int value = I;
+};
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // ------------------------------------------------------------------ fp32 contract
 constexpr float kHalfPi = 0x1.921fb6p+0f;
 constexpr float kPi = 0x1.921fb6p+1f;

@@ -8,6 +8,10 @@
 #ifndef PV_PK_SPLIT
 #define PV_PK_SPLIT 0  // packed-instruction real split (analysis): measured slower (latency)
 #endif
+#ifndef PV_SPLIT_BP
+#define PV_SPLIT_BP 1  // analysis real split from the last pass's registers via ds_bpermute
+                       // (split_chunk_bp) instead of a final image in LDS (split_chunk)
+#endif
 #ifndef PV_PK_PRESTEP
 #define PV_PK_PRESTEP 1  // packed-instruction inverse real-FFT pre-step (synthesis)
 #endif
@@ -95,6 +99,65 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
         X[c] = make_float2(Xr, Xi);
     }
 #endif
+}
+
+// register index holding slot c after the last FFT pass (inverse of last_slot)
+template <int L>
+constexpr int slot_reg(int c) {
+    for (int idx = 0; idx < Geo<L>::E; ++idx)
+        if (last_slot<L>(idx) == c) return idx;
+    return -1;
+}
+
+// split_chunk from the last FFT pass's registers instead of the natural-order image in LDS
+// (no final tile store, no tile reads): lane l holds Z[l + 64 c] in register slot_reg(c), so
+// A = Z[k], k = l + 64 i, is the lane's own register and B = Z[(L - k) mod L] =
+// Z[(64 - l) + 64 (E - 1 - i)] is register slot E-1-i of lane 64 - l — a lane reversal by
+// ds_bpermute (crossbar only).  Lane 0's partners are its own registers (Z[(L - 64 i) mod L]
+// = slot (E - i) mod E): it selects them before the permute and reads from itself.  Same
+// operands, same operations as split_chunk: bit-identical bins.
+template <int L, int CH, bool TWICE, int I0>
+__device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], const float2* twsl, int lane,
+                                               float2 (&X)[CH]) {
+    constexpr int E = Geo<L>::E;
+    const int rev = ((64 - lane) & 63) << 2;
+    const bool l0 = lane == 0;
+    const float2* baseT = twsl + lane;
+    float2 A[CH], Bz[CH], tw[CH];
+    static_for<0, CH>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int i = I0 + c;
+        if constexpr (i < E) {
+            A[c] = v[slot_reg<L>(i)];
+            const float2 o = v[slot_reg<L>(E - 1 - i)];
+            const float2 m = v[slot_reg<L>((E - i) & (E - 1))];
+            const float sx = l0 ? m.x : o.x, sy = l0 ? m.y : o.y;
+            Bz[c].x = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sx)));
+            Bz[c].y = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sy)));
+            tw[c] = lds_ld(&baseT[64 * i]);
+        } else {
+            // bin L, computed by every lane (all store the same value to one address):
+            // A = B = Z[0], lane 0's slot 0, broadcast
+            const float2 z0 = v[slot_reg<L>(0)];
+            A[c] = make_float2(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z0.x))),
+                               __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z0.y))));
+            Bz[c] = A[c];
+            tw[c] = lds_ld(&twsl[L]);
+        }
+    });
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int i = I0 + c;
+        constexpr float h = TWICE ? 1.0f : 0.5f;
+        const float er = h * (A[c].x + Bz[c].x);
+        const float ei = h * (A[c].y - Bz[c].y);
+        const float orr = h * (A[c].y + Bz[c].y);
+        const float oi = h * (Bz[c].x - A[c].x);
+        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
+        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
+        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
+        X[c] = make_float2(Xr, Xi);
+    }
 }
 
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)

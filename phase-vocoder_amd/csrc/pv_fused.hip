@@ -21,6 +21,11 @@
 // second of the two workgroups to finish (no k_seam launch).
 #include "pv_syn_run.hpp"
 
+#ifndef PV_FUSED_SPLIT_BP
+#define PV_FUSED_SPLIT_BP 0  // the register split (split_chunk_bp) costs this kernel 2 VGPRs over
+                             // 128 at L = 512 (3 waves/SIMD, or spills at 4): config 2 +2-3 %
+#endif
+
 namespace pv {
 
 // Inter-workgroup hand-offs: st_sc1 / ld_sc1 / arrive / close_seams_inline (pv_syn_run.hpp),
@@ -138,14 +143,15 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
             }
             if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
             // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv
-            fft_run<L, false>(z, tile, twl, tw0, lane);
+            fft_run<L, false, !PV_FUSED_SPLIT_BP>(z, tile, twl, tw0, lane);
             float2 sv[E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
             constexpr int CH = 3;
-#pragma unroll
-            for (int i0 = 0; i0 <= E; i0 += CH) {
+            static_for<0, (E + CH) / CH>([&](auto ic) {
+                constexpr int i0 = decltype(ic)::value * CH;
                 float2 X[CH];
-                split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
+                if constexpr ((bool)PV_FUSED_SPLIT_BP) split_chunk_bp<L, CH, true, i0>(z, twsl, lane, X);
+                else split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
 #pragma unroll
                 for (int c2 = 0; c2 < CH; ++c2) {
                     const int i = i0 + c2;
@@ -157,8 +163,8 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
                     // bin L (i = E): the same value and address on every lane
                     __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
                 }
-            }
-            wave_lds_sync();  // split reads done before the synthesis reuses the tile
+            });
+            wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers
             synth_frame<L, MODE, false, true, false, false, true>(sv, false, 0u, M, phprev, pmap, stb, tw0, tile,
                                                                   lane, z, ekr, jkr);

@@ -119,16 +119,17 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
                 z[q].y = xv.y * wv.y;
             }
         }
-        fft_run<L, false>(z, tile, twl, tw0, lane);
+        fft_run<L, false, !PV_SPLIT_BP>(z, tile, twl, tw0, lane);  // PV_SPLIT_BP: the split reads the registers
         float2 sv[E + 1];
         float2* srow = (p.spec != nullptr)
                            ? p.spec + (long long)c * p.ld_spec + (long long)f * p.spec_stride
                            : nullptr;
         constexpr int CH = 3;
-#pragma unroll
-        for (int i0 = 0; i0 <= E; i0 += CH) {
+        static_for<0, (E + CH) / CH>([&](auto ic) {
+            constexpr int i0 = decltype(ic)::value * CH;
             float2 X[CH];
-            split_chunk<L, CH>(tile, twsl, lane, i0, X);
+            if constexpr ((bool)PV_SPLIT_BP) split_chunk_bp<L, CH, false, i0>(z, twsl, lane, X);
+            else split_chunk<L, CH, false>(tile, twsl, lane, i0, X);
 #pragma unroll
             for (int c2 = 0; c2 < CH; ++c2) {
                 const int i = i0 + c2;
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
                 sv[i] = make_float2(mag, ph);
                 if (srow != nullptr && (i < E || lane == 0)) srow[(i == E) ? L : lane + 64 * i] = sv[i];
             }
-        }
+        });
         wave_lds_sync();
         // ---- processing + resynthesis: time samples to tile (natural order)
         const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
