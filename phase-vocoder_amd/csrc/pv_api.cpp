@@ -660,10 +660,14 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     // ---- single-launch path (q = 1): no halo frame, so runs can be as short as the overlap
     // tail allows (F hs >= N - hs) to give a single stream enough waves; PV_FUSED=0 disables
     // it (A/B), PV_FUSED_FRAMES overrides its run length
-    // PV_FUSED_FORCE=1 (timing probe only, output WRONG for q > 1): runs the q = 1 kernel on
-    // any STANDARD geometry to bound what a single-launch path could reach there
+#ifdef PV_TIMING_PROBES
+    // PV_FUSED_FORCE=1 (timing probe builds only, output WRONG for q > 1): runs the q = 1
+    // kernel on any STANDARD geometry to bound what a single-launch path could reach there
     const char* ff = std::getenv("PV_FUSED_FORCE");
     const bool force_fused = ff && ff[0] == '1';
+#else
+    const bool force_fused = false;
+#endif
     if (h->mode == PV_MODE_STANDARD && (h->q == 1 || force_fused) && pv::fused_supported(h->L_syn, h->hs)) {
         const int fmin = std::max(2, (h->tail_len + h->hs - 1) / h->hs);
         int Ff = (int)std::min<long long>(h->F, std::max<long long>(fmin, work / 4096));
