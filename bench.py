@@ -137,8 +137,9 @@ def oracle_check(x, out_rows, idx, N, hop_div, effect, scale, frames, all_finite
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 10; 200 for the 50-us c2 step, 2000 callbacks for rt)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 20 for c2)")
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the timed CPU baseline")
@@ -150,6 +151,11 @@ def main():
                          "single 60 s stream, pitch 2.0; c4: configs[3] per-GPU slice (1024 ch, "
                          "N=2048 hop=512, pitch 1.5); rt: configs[4] real-time mode")
     args = ap.parse_args()
+    # a c2 step is ~50 us: 10 steps would time the barrier/synchronise bracket, not the path
+    if args.steps is None:
+        args.steps = 200 if args.workload == "c2" else 10
+    if args.warmup is None:
+        args.warmup = 20 if args.workload == "c2" else 3
     if args.workload == "rt":
         return bench_rt(args)
 

@@ -89,6 +89,7 @@ void split_twiddles(int N, std::vector<float2>& t) {
 struct Profile {
     bool enabled = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
+    std::vector<hipEvent_t> pool;  // read-out events, reused (hipEventCreate per launch costs µs)
     std::vector<int> ev_kernel;
     double total_ms[kNumKernels] = {0};
     int launches[kNumKernels] = {0};
@@ -145,8 +146,18 @@ struct DeviceGuard {
 pv_status prof_begin(pv_handle* h, int kernel, hipStream_t s) {
     if (!h->prof.enabled) return PV_OK;
     hipEvent_t a, b;
-    PV_HIP(hipEventCreate(&a));
-    PV_HIP(hipEventCreate(&b));
+    auto take = [&](hipEvent_t* e) -> pv_status {
+        if (!h->prof.pool.empty()) {
+            *e = h->prof.pool.back();
+            h->prof.pool.pop_back();
+            return PV_OK;
+        }
+        PV_HIP(hipEventCreate(e));
+        return PV_OK;
+    };
+    pv_status st = take(&a);
+    if (st == PV_OK) st = take(&b);
+    if (st != PV_OK) return st;
     PV_HIP(hipEventRecord(a, s));
     h->prof.ev_start.push_back(a);
     h->prof.ev_stop.push_back(b);
@@ -488,6 +499,7 @@ void pv_destroy(pv_handle* h) {
         if (p) (void)hipFree(p);
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
     for (auto e : h->prof.ev_stop) (void)hipEventDestroy(e);
+    for (auto e : h->prof.pool) (void)hipEventDestroy(e);
     delete h;
 }
 
@@ -904,6 +916,14 @@ pv_status pv_check_device(pv_handle* h) {
 pv_status pv_profile_enable(pv_handle* h, int enable) {
     if (!h) return fail(PV_ERR_ARG, "null handle");
     h->prof.enabled = enable != 0;
+    if (h->prof.enabled) {  // events for the first launches, created here, not per launch
+        DeviceGuard g(h->cfg.device);
+        while (h->prof.pool.size() < 512) {
+            hipEvent_t e;
+            PV_HIP(hipEventCreate(&e));
+            h->prof.pool.push_back(e);
+        }
+    }
     return PV_OK;
 }
 
@@ -917,8 +937,8 @@ int pv_profile_read(pv_handle* h, const char** names, double* total_ms, int* lau
             h->prof.total_ms[h->prof.ev_kernel[i]] += ms;
             h->prof.launches[h->prof.ev_kernel[i]] += 1;
         }
-        (void)hipEventDestroy(h->prof.ev_start[i]);
-        (void)hipEventDestroy(h->prof.ev_stop[i]);
+        h->prof.pool.push_back(h->prof.ev_start[i]);
+        h->prof.pool.push_back(h->prof.ev_stop[i]);
     }
     h->prof.ev_start.clear();
     h->prof.ev_stop.clear();
