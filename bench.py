@@ -328,8 +328,9 @@ def main():
 def bench_rt(args):
     """BASELINE configs[4]: real-time ring-buffer mode, 256 channels, N=256, hop=64
     (64-sample callbacks at 44.1 kHz: 1.451 ms deadline), PV_STANDARD pitch shift 1.5,
-    one hipGraph replay per callback (pinned host in -> device -> kernel -> pinned host
-    out).  A step = one synchronous callback; latency percentiles are host wall-clock per
+    one kernel per callback reading / writing pinned host buffers in place (zero-copy; a
+    direct launch: the captured one-node hipGraph replay measured 28 vs 21 us p50,
+    PV_RT_LAUNCH=graph selects it).  A step = one synchronous callback; latency percentiles are host wall-clock per
     callback (what an RtAudio thread waits for)."""
     import torch
     from pvamd import PITCH_SHIFT, RealTimeVocoder
@@ -376,7 +377,8 @@ def bench_rt(args):
         "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (3 sines + noise), 64-sample blocks cycled",
         "config": {"workload": "BASELINE configs[4]: real-time ring buffer, 256 ch, N=256 hop=64, "
-                               "PV_STANDARD pitch 1.5, hipGraph per callback",
+                               "PV_STANDARD pitch 1.5, one zero-copy launch per callback ("
+                               + os.environ.get("PV_RT_LAUNCH", "direct") + ")",
                    "channels": C, "N": N, "hop": hop, "out_hop": rt.outHopSize},
         "latency_us": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                        "max": float(lat.max()), "deadline": deadline_us,

@@ -92,7 +92,11 @@ def test_rt_many_channels_and_batch_equivalence(cuda):
         assert rms(g[c], ref[:K * hop]) <= RMS_TOL
 
 
-def test_rt_graph_callback_equals_push_and_reset(cuda):
+@pytest.mark.parametrize("launch", ["direct", "graph"])
+def test_rt_graph_callback_equals_push_and_reset(cuda, monkeypatch, launch):
+    """The synchronous callback (direct launch by default, or the captured hipGraph replay)
+    equals the plain push, and reset restarts the stream."""
+    monkeypatch.setenv("PV_RT_LAUNCH", launch)
     N, hop_div, C, K = 256, 4, 8, 30
     hop = N // hop_div
     xs = np.stack([synth(K * hop, 900 + c) for c in range(C)])
