@@ -328,9 +328,10 @@ def main():
 def bench_rt(args):
     """BASELINE configs[4]: real-time ring-buffer mode, 256 channels, N=256, hop=64
     (64-sample callbacks at 44.1 kHz: 1.451 ms deadline), PV_STANDARD pitch shift 1.5,
-    one kernel per callback reading / writing pinned host buffers in place (zero-copy; a
-    direct launch: the captured one-node hipGraph replay measured 28 vs 21 us p50,
-    PV_RT_LAUNCH=graph selects it).  A step = one synchronous callback; latency percentiles are host wall-clock per
+    one hipGraph replay per callback (BASELINE config 5's form; the graph's one kernel node
+    reads / writes the pinned host buffers in place).  The same callbacks are then timed with
+    a direct launch per callback (`alt_direct_launch`: measured faster on ROCm 7.2).  A step
+    = one synchronous callback; latency percentiles are host wall-clock per
     callback (what an RtAudio thread waits for)."""
     import torch
     from pvamd import PITCH_SHIFT, RealTimeVocoder
@@ -343,19 +344,33 @@ def bench_rt(args):
     hop = rt.hopSize
     steps = args.steps if args.steps != 10 else 2000
     warm = max(args.warmup, 50)
-    rt.capture(1)
     blocks = synth_channels_np(C, hop * 64, 20240, cpu_share()[0]).reshape(C, 64, hop)
-    for j in range(warm):
-        rt.host_in[:] = blocks[:, j % 64]
-        rt.callback()
-    lat = np.empty(steps)
-    t0 = time.perf_counter()
-    for j in range(steps):
-        a = time.perf_counter_ns()
-        rt.host_in[:] = blocks[:, j % 64]          # main.cpp:49 memcpy into curr_input
-        rt.callback()
-        lat[j] = (time.perf_counter_ns() - a) * 1e-3
-    dt = time.perf_counter() - t0
+
+    def run_callbacks(v):
+        for j in range(warm):
+            v.host_in[:] = blocks[:, j % 64]
+            v.callback()
+        lat = np.empty(steps)
+        t0 = time.perf_counter()
+        for j in range(steps):
+            a = time.perf_counter_ns()
+            v.host_in[:] = blocks[:, j % 64]          # main.cpp:49 memcpy into curr_input
+            v.callback()
+            lat[j] = (time.perf_counter_ns() - a) * 1e-3
+        return lat, time.perf_counter() - t0
+
+    prev = os.environ.pop("PV_RT_LAUNCH", None)
+    rt.capture(1)                                  # hipGraph replay per callback (config 5)
+    lat, dt = run_callbacks(rt)
+    os.environ["PV_RT_LAUNCH"] = "direct"          # the same callbacks, one launch each
+    alt = RealTimeVocoder(N, PITCH_SHIFT, scale, hop_div, channels=C, device=local)
+    alt.capture(1)
+    lat_d, dt_d = run_callbacks(alt)
+    alt.close()
+    if prev is None:
+        os.environ.pop("PV_RT_LAUNCH", None)
+    else:
+        os.environ["PV_RT_LAUNCH"] = prev
     # device time of the per-callback kernel alone (events on the push stream)
     x = torch.from_numpy(blocks[:, 0].copy()).cuda()
     out = torch.empty((C, rt.outHopSize), device="cuda")
@@ -377,13 +392,14 @@ def bench_rt(args):
         "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (3 sines + noise), 64-sample blocks cycled",
         "config": {"workload": "BASELINE configs[4]: real-time ring buffer, 256 ch, N=256 hop=64, "
-                               "PV_STANDARD pitch 1.5, one zero-copy launch per callback ("
-                               + os.environ.get("PV_RT_LAUNCH", "direct") + ")",
+                               "PV_STANDARD pitch 1.5, hipGraph replay per callback (zero-copy)",
                    "channels": C, "N": N, "hop": hop, "out_hop": rt.outHopSize},
         "latency_us": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                        "max": float(lat.max()), "deadline": deadline_us,
                        "missed": int(np.sum(lat > deadline_us))},
         "kernel_us": k_us,
+        "alt_direct_launch": {"value": C * steps / dt_d, "p50_us": float(np.percentile(lat_d, 50)),
+                              "p99_us": float(np.percentile(lat_d, 99)), "max_us": float(lat_d.max())},
         "roofline": {"bound": "latency", "kernel": "rt", "achieved": C * frame_bytes / (k_us * 1e-6) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": C * frame_bytes / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None},

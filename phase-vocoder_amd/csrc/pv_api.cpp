@@ -981,8 +981,9 @@ struct pv_rt {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     float *m_in = nullptr, *m_out = nullptr;  // device views of h_in / h_out (zero-copy)
-    int direct = 0;  // launch pv_rt_push per callback (default: measured p50 21 vs 28 us for the
-                     // one-node graph replay on ROCm 7.2); PV_RT_LAUNCH=graph replays the graph
+    int direct = 0;  // PV_RT_LAUNCH=direct: launch pv_rt_push per callback instead of replaying
+                     // the captured graph (BASELINE config 5's form, the default): measured p50
+                     // 21 vs 28 us per callback on ROCm 7.2
     int spin = 0;    // PV_RT_WAIT=spin: poll the stream instead of a blocking synchronise
 };
 
@@ -1180,7 +1181,7 @@ pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     rt->m_in = zero_copy ? m_in : nullptr;
     rt->m_out = zero_copy ? m_out : nullptr;
     const char* lv = std::getenv("PV_RT_LAUNCH");
-    rt->direct = (zero_copy && !(lv && std::string(lv) == "graph")) ? 1 : 0;
+    rt->direct = (zero_copy && lv && std::string(lv) == "direct") ? 1 : 0;
     const char* wv = std::getenv("PV_RT_WAIT");
     rt->spin = (wv && std::string(wv) == "spin") ? 1 : 0;
     return PV_OK;
