@@ -908,7 +908,10 @@ pv_status pv_check_device(pv_handle* h) {
     if (h->d_chain_err) {
         int err = 0;
         PV_HIP(hipMemcpy(&err, h->d_chain_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (err) return fail(PV_ERR_HIP, "chained path: a run-group record never arrived (output invalid)");
+        if (err) {
+            PV_HIP(hipMemset(h->d_chain_err, 0, sizeof(int)));  // reported once
+            return fail(PV_ERR_HIP, "chained path: a run-group record never arrived (output invalid)");
+        }
     }
     return PV_OK;
 }
