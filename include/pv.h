@@ -43,7 +43,8 @@ extern "C" {
 #endif
 
 #define PV_ABI_VERSION 3  /* 2: pv_config.window / nan_faithful, pv_set_window;
-                             3: pv_info.single_launch / single_launch_frames, pv_check_device */
+                             3: pv_info.single_launch / single_launch_frames / lane_constants,
+                                pv_check_device */
 
 typedef struct pv_handle pv_handle;
 
@@ -108,6 +109,10 @@ typedef struct pv_info {
                                  launch chained over run groups (q = 2^e, pv_chain.hip; an
                                  unaligned input falls back to the split path)            */
     int single_launch_frames; /* frames per run of that launch (0 for the split path)     */
+    int lane_constants;       /* 1: the split synthesis keeps the per-bin unwrap constants
+                                 in registers (e_k and (p j_k) mod q repeat every 64 bins:
+                                 64 a multiple of N / hop and q of 64 hop / N, e.g. config
+                                 3 and 4); PV_SYN_LANEK=0 read by pv_create turns it off  */
 } pv_info;
 
 int pv_abi_version(void);

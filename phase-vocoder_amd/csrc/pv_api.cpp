@@ -108,6 +108,7 @@ struct pv_handle {
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
     int q_pow2 = 1;
+    int k_lane = 0;  // e_k and (p j_k) mod q depend on k mod 64 only (synthesis LANEK kernels)
     // device tables
     float *d_win = nullptr, *d_gain = nullptr, *d_ek = nullptr;
     float2 *d_tw_ana = nullptr, *d_tws_ana = nullptr, *d_tw_syn = nullptr, *d_tws_syn = nullptr;
@@ -293,6 +294,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.out_aligned = ((reinterpret_cast<uintptr_t>(out) & 7) == 0) && ((ldo & 1) == 0);
     p.tails = h->d_tails;
     p.tail_len = h->tail_len;
+    p.k_lane = h->k_lane;
     const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
     PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, smode, C, p, s));
     const int nwg = (nruns + 3) / 4;
@@ -485,6 +487,7 @@ pv_status pv_get_info(const pv_handle* h, pv_info* info) {
     info->scale = h->scale;
     info->single_launch = h->F_fused > 0 ? 1 : h->F_chain > 0 ? 2 : 0;
     info->single_launch_frames = h->F_fused > 0 ? h->F_fused : h->F_chain;
+    info->lane_constants = h->k_lane;
     return PV_OK;
 }
 
@@ -654,6 +657,17 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     }
     if ((st = upload(&h->d_ek, ek)) != PV_OK) return bail(st);
     if ((st = upload(&h->d_jk_mod, jkm)) != PV_OK) return bail(st);
+    {
+        // per-lane unwrap constants (the synthesis keeps them in two registers): every bin
+        // k < L repeats bin k mod 64, and bin L's e equals bin 0's
+        const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
+        bool kl = B > 64 && ek[B - 1] == ek[0] &&
+                  pv::synthesis_lane_kernel(h->L_syn, smode, h->hs, h->q_pow2 != 0, h->q);
+        for (int k = 64; kl && k < B - 1; ++k) kl = (ek[k] == ek[k & 63]) && (jkm[k] == jkm[k & 63]);
+        if (const char* ev = std::getenv("PV_SYN_LANEK"))
+            if (ev[0] == '0') kl = false;
+        h->k_lane = kl ? 1 : 0;
+    }
 
     // ---- pitch map: k' = floor(beta*k + 0.5) (magnitudes summed, phase from smallest k)
     std::vector<int> first(B, -1), cnt(B, 0);

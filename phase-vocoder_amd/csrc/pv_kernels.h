@@ -57,6 +57,7 @@ struct SynParams {
     int out_aligned;                   // out base and ldo allow 8-byte vector stores
     float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
     int tail_len;
+    int k_lane;                        // e_k, (p j_k) mod q depend on k mod 64 only (syn_run LANEK)
 };
 
 // single-launch STANDARD path for q = 1 (pv_fused.hip)
@@ -152,6 +153,9 @@ hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipSt
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
+// the synthesis kernel for this geometry can take SynParams.k_lane (register overlap-add,
+// power-of-two q, STANDARD)
+bool synthesis_lane_kernel(int L, int mode, int hs, bool q_pow2, unsigned long long q);
 hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
 bool fused_supported(int L, int hs);
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s);

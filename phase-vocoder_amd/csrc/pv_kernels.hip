@@ -126,7 +126,7 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 #ifndef PV_SYN_WAVES1024
 #define PV_SYN_WAVES1024 1  // waves per SIMD the L = 1024 synthesis is compiled for
 #endif
-template <int L, int MODE, int DT, bool QPOW2 = false>
+template <int L, int MODE, int DT, bool QPOW2 = false, bool LANEK = false>
 __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 : (L == 1024) ? PV_SYN_WAVES1024 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     }
     constexpr int NS = SynTraits<L, MODE, DT, QPOW2>::NS, D = SynTraits<L, MODE, DT, QPOW2>::D;
     float2 acc[NS];
-    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, false>(
+    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, false, LANEK>(
         p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, false, M, phprev, acc);
     if constexpr (ROLA) {
         // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
@@ -354,13 +354,17 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
 // hop) for all overlap-add variants; the generic-q path uses the LDS ring (DT = 0).
 template <int MODE, bool QP>
 static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParams& p, hipStream_t s) {
-#define PV_SYN_DT(LL_)                                                                                    \
+#define PV_SYN_DT1(LL_, KL_)                                                                              \
     switch (dt) {                                                                                         \
-        case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1, QP>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
-        case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2, QP>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
-        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
+        case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1, QP, KL_>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
+        case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2, QP, KL_>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
+        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP, KL_>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
         default: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0, QP>), grid, dim3(256), syn_lds<LL_>(0), s, p); break; \
     }
+    // per-lane unwrap constants: register overlap-add STANDARD kernels (QP, MODE != 1)
+#define PV_SYN_DT(LL_)                                        \
+    if (QP && MODE != 1 && p.k_lane) { PV_SYN_DT1(LL_, (QP && MODE != 1)) } \
+    else { PV_SYN_DT1(LL_, false) }
 #define PV_SYN_DT0(LL_) hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0, QP>), grid, dim3(256), syn_lds<LL_>(0), s, p)
     if constexpr (QP || MODE == 1) {
         switch (L) {
@@ -382,8 +386,14 @@ static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParam
         }
     }
 #undef PV_SYN_DT
+#undef PV_SYN_DT1
 #undef PV_SYN_DT0
     return hipGetLastError();
+}
+
+bool synthesis_lane_kernel(int L, int mode, int hs, bool q_pow2, unsigned long long q) {
+    const bool qp = q_pow2 && q <= (PV_REV_ACC ? 4096ull : (1ull << 24));
+    return mode != 1 && qp && syn_dt(L, hs) != 0;
 }
 
 // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT

@@ -150,7 +150,11 @@ struct SynTraits {
 // NTROW: spectrum rows loaded non-temporally.  HEADSC1: the positions < N - hs of a run
 // whose workgroup has a predecessor (head) are stored write-through (sc1) for an in-kernel
 // seam hand-off; `head` says whether this wave's run is such a head.
-template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool HEADSC1>
+// LANEK: the unwrap constants are per-lane (e_k and (p j_k) mod q depend on k mod 64 only:
+// 64 a multiple of the hop divisor and q of 64 / hop divisor, checked by the host —
+// config 3 and 4): two registers (and bin L's j constant) instead of two LDS reads per bin
+// and frame.
+template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool HEADSC1, bool LANEK = false>
 __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, const float2 (&tw0)[Geo<L>::E],
                                         int lane, int w, int c, int t0, int nfr, bool head,
                                         int (&M)[Geo<L>::E + 1], float (&phprev)[Geo<L>::E + 1],
@@ -188,10 +192,21 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
 
     // unwrap constants of the lane's bins in registers for the whole run (ROLA kernels
     // have VGPRs to spare below their LDS-bound occupancy)
-    constexpr bool KREG = ROLA && MODE == 0 && PV_SYN_KREG;  // pitch (MODE 2) would spill
+    constexpr bool KREG = (ROLA && MODE == 0 && PV_SYN_KREG) || (LANEK && MODE != 1);  // (MODE 2 would spill)
     float ekr[E + 1];
     unsigned jkr[E + 1];
-    if constexpr (KREG) PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&sc.ekl[k]); jkr[i] = lds_ld(&sc.jkl[k]); })
+    if constexpr (LANEK && MODE != 1) {
+        const float e_lane = lds_ld(&sc.ekl[lane]);
+        const unsigned j_lane = lds_ld(&sc.jkl[lane]);
+        const unsigned j_last = lds_ld(&sc.jkl[L]);  // bin L (lane 0)
+#pragma unroll
+        for (int i = 0; i <= E; ++i) {
+            ekr[i] = e_lane;  // e_L = e_0: lane 0 is the only one that uses bin L
+            jkr[i] = (i == E) ? j_last : j_lane;
+        }
+    } else if constexpr (KREG) {
+        PV_FOR_BINS(E, lane, { ekr[i] = lds_ld(&sc.ekl[k]); jkr[i] = lds_ld(&sc.jkl[k]); })
+    }
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
                         (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};

@@ -35,7 +35,8 @@ class pv_info(ctypes.Structure):
                 ("spec_bins", ctypes.c_int), ("spec_stride", ctypes.c_int),
                 ("frames_per_run", ctypes.c_int), ("mode", ctypes.c_int), ("effect", ctypes.c_int),
                 ("scale", ctypes.c_float), ("single_launch", ctypes.c_int),
-                ("single_launch_frames", ctypes.c_int)]
+                ("single_launch_frames", ctypes.c_int),
+                ("lane_constants", ctypes.c_int)]
 
 
 _lib = None

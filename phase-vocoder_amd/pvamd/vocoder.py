@@ -75,6 +75,7 @@ class PhaseVocoder:
         # 0 split path, 1 single q = 1 launch, 2 single launch chained over run groups
         self.single_launch = info.single_launch
         self.single_launch_frames = info.single_launch_frames
+        self.lane_constants = info.lane_constants
 
     @classmethod
     def single_arg(cls, samples: int, **kw):
