@@ -297,21 +297,30 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             float2 Y[E + 1];
             PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
             wave_lds_sync();
-            PV_FOR_BINS(E, lane, {
-                // {first source, count} in one 8-byte read; the first source's {mag, phase}
-                // in one read, without a branch (zero when no source maps here); more
-                // sources (ratios < 1) are summed in order like the oracle
-                const i2v sc = lds_ld2i(&srcl[2 * k]);
-                const int s = sc.x, cnt = sc.y;
-                const float2 f = lds_ld(&tile[G_::pad(s >= 0 ? s : 0)]);
-                float ms = (s >= 0) ? f.x : 0.0f;
-                const float pc = (s >= 0) ? f.y : 0.0f;
-                if (pm.multi)  // wave-uniform: ratios >= 1 never enter the loop
-                    for (int qq = 1; qq < cnt; ++qq) ms += tile[G_::pad(s + qq)].x;
-                float sn, cs;
-                sincos_rev(pc, &sn, &cs);
-                Y[i] = make_float2(ms * cs, ms * sn);
+            // {first source, count} in one 8-byte read; the first source's {mag, phase}
+            // in one read, without a branch (zero when no source maps here); more sources
+            // (ratios < 1) are summed in order like the oracle.  The ratio test is hoisted
+            // out of the bin loop (wave-uniform): inside it the compiler merges it with the
+            // per-lane count test into an exec-masked branch per bin (17 at L = 1024).
+#define PV_PITCH_GATHER(MULTI_)                                                   \
+            PV_FOR_BINS(E, lane, {                                                \
+                const i2v sc = lds_ld2i(&srcl[2 * k]);                            \
+                const int s = sc.x;                                               \
+                const float2 f = lds_ld(&tile[G_::pad(s >= 0 ? s : 0)]);          \
+                float ms = (s >= 0) ? f.x : 0.0f;                                 \
+                const float pc = (s >= 0) ? f.y : 0.0f;                           \
+                if (MULTI_)                                                       \
+                    for (int qq = 1; qq < sc.y; ++qq) ms += tile[G_::pad(s + qq)].x; \
+                float sn, cs;                                                     \
+                sincos_rev(pc, &sn, &cs);                                         \
+                Y[i] = make_float2(ms * cs, ms * sn);                             \
             })
+            if (pm.multi) {
+                PV_PITCH_GATHER(true)
+            } else {
+                PV_PITCH_GATHER(false)
+            }
+#undef PV_PITCH_GATHER
             wave_lds_sync();
             PV_FOR_BINS(E, lane, {
                 float2 y = Y[i];
