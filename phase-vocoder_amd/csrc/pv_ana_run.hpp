@@ -28,6 +28,17 @@
 #ifndef PV_ANA_PF2
 #define PV_ANA_PF2 0  // analysis input prefetch distance 2 (shifted-register path)
 #endif
+#ifndef PV_ANA_TWSHARE
+#define PV_ANA_TWSHARE 1  // L = 1024: the last pass's twiddles from the split table (fft_pass
+                          // TWS_MIN), 6 KB less LDS: 3 workgroups per CU instead of 2
+#endif
+namespace pv {
+template <int L>
+constexpr int ana_tws_min() { return (PV_ANA_TWSHARE && L == 1024) ? L / 4 : 0; }
+// stage-major twiddle entries the analysis keeps in LDS
+template <int L>
+constexpr int ana_twl_n() { return ana_tws_min<L>() > 0 ? ana_tws_min<L>() : L; }
+}  // namespace pv
 #ifndef PV_ANA_CH
 #define PV_ANA_CH 3  // analysis: bins per batch of LDS reads + atan2 chains
 #endif
@@ -96,7 +107,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         wave_lds_sync();
 #else
         // SPLIT_BP: the last pass's registers feed the split directly (no final image)
-        fft_run<L, false, !SPLIT_BP>(z, tile, twl, tw0, lane);
+        fft_run<L, false, !SPLIT_BP, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
 #endif
         // bins in chunks of CH (bounded live registers), all reads of a chunk batched
         constexpr int CH = PV_ANA_CH;

@@ -17,18 +17,22 @@ namespace pv {
 #ifndef PV_ANA_WAVES512
 #define PV_ANA_WAVES512 4
 #endif
+#ifndef PV_ANA_WAVES1024
+#define PV_ANA_WAVES1024 3  // 154 VGPRs; LDS (with PV_ANA_TWSHARE) allows 3 workgroups per CU
+#endif
 // D > 0: hop = 128 D samples, so frame u+1's register q is frame u's register q + D and a
 // frame costs only its D new sample pairs per lane (the other E - D are shifted in
 // registers): 1/E of the frame's bytes leave L2 instead of all of them.
 template <int L, bool EKL, int D = 0>
-__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? 2 : 1) void k_std_analysis(AnaParams p) {
+__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? PV_ANA_WAVES1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int B = L + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* twl = reinterpret_cast<float2*>(smem);   // L   stage-major twiddles
-    float2* twsl = twl + L;                           // L+1 split twiddles (+1 pad)
+    constexpr int TWN = ana_twl_n<L>();
+    float2* twl = reinterpret_cast<float2*>(smem);   // TWN stage-major twiddles (L, or L/4)
+    float2* twsl = twl + TWN;                         // L+1 split twiddles (+1 pad)
     float2* tiles = twsl + (L + 2);                   // 4 x TILE
     float* winl = reinterpret_cast<float*>(tiles + 4 * G_::TILE);  // N
     float* ekl = winl + N;                            // B
@@ -41,7 +45,7 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
 #endif
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
-    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
+    for (int i = tid; i < TWN; i += 256) twl[i] = p.tw[i];
     for (int i = tid; i < B; i += 256) {
         twsl[i] = p.tws[i];
         if (EKL) ekl[i] = p.ek[i];
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
 // ------------------------------------------------------------------ launchers
 template <int L>
 static size_t ana_lds_std(bool ekl) {
-    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
+    return sizeof(float2) * (ana_twl_n<L>() + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
 }
 template <int L>
 static size_t ana_lds_compat() {

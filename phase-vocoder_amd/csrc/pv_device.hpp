@@ -399,9 +399,15 @@ static_assert(Geo<128>::layouts_affine() && Geo<256>::layouts_affine() && Geo<51
 // One register pass: P-th pass, INV selects conjugated twiddles.
 // Input layout : v[g*R + q] = x[j + q*L/R],   j = lane + 64 g
 // Output layout: v[g*R + f] = y[(j/S)*R*S + j%S + S*bitrev_r(f)]
-template <int L, int P, bool INV>
+// TWS_MIN > 0: stages Ns >= TWS_MIN read W(m, Ns) = e^{-2 pi i m / 2Ns} from the split
+// table tws (e^{-2 pi i k / 2L}, k <= L) at k = m L / Ns instead of the stage-major table:
+// both are tw_entry() of the same double angle (2 pi m / 2Ns and 2 pi (m L/Ns) / 2L differ
+// by a power-of-two scaling of numerator and denominator, exact), so the values are the
+// same bits and the stage-major table only needs its first TWS_MIN - 1 entries in LDS.
+template <int L, int P, bool INV, int TWS_MIN = 0>
 __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* tw,
-                                         const float2 (&tw0)[Geo<L>::E], int lane) {
+                                         const float2 (&tw0)[Geo<L>::E], int lane,
+                                         const float2* tws = nullptr) {
     using G_ = Geo<L>;
     constexpr int S = 1 << (P * G_::RLOG);
     constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
@@ -451,7 +457,8 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                     const float2 w = tw0[(Ns - 1) + br];
                     t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
                 } else {
-                    const float2 w = lds_ld(&tw[(Ns - 1) + jm + S * br]);
+                    const float2 w = (TWS_MIN > 0 && Ns >= TWS_MIN) ? lds_ld(&tws[(jm + S * br) * (L / Ns)])
+                                                                    : lds_ld(&tw[(Ns - 1) + jm + S * br]);
                     t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
                 }
                 b[2 * s] = top + t;
@@ -515,16 +522,17 @@ __device__ __forceinline__ void load_tw0(float2 (&tw0)[Geo<L>::E], const float2*
 // STORE_LAST the result is left in `tile` in natural order (padded indexing); without it
 // the last pass's output stays in v, where register v[g*R + f] holds point
 // lane + 64 g + S_last * bitrev_r(f)  (= lane + 64 c, see last_slot()).
-template <int L, bool INV, bool STORE_LAST = true, int P = 0>
+template <int L, bool INV, bool STORE_LAST = true, int P = 0, int TWS_MIN = 0>
 __device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, const float2* tw,
-                                        const float2 (&tw0)[Geo<L>::E], int lane) {
-    fft_pass<L, P, INV>(v, tw, tw0, lane);
+                                        const float2 (&tw0)[Geo<L>::E], int lane,
+                                        const float2* tws = nullptr) {
+    fft_pass<L, P, INV, TWS_MIN>(v, tw, tw0, lane, tws);
     if constexpr (P + 1 < Geo<L>::NPASS) {
         pass_store<L, P>(v, tile, lane);
         wave_lds_sync();
         pass_load<L, P + 1>(v, tile, lane);
         wave_lds_sync();
-        fft_run<L, INV, STORE_LAST, P + 1>(v, tile, tw, tw0, lane);
+        fft_run<L, INV, STORE_LAST, P + 1, TWS_MIN>(v, tile, tw, tw0, lane, tws);
     } else if constexpr (STORE_LAST) {
         pass_store<L, P>(v, tile, lane);
         wave_lds_sync();
