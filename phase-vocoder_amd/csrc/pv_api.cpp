@@ -570,6 +570,10 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     const long long work = (long long)std::max(cfg->max_channels, 1) * std::max(cfg->max_frames, 1);
     // (measured on config 3: F = 32 / 48 / 64 / 96 -> 3.64 / 3.74 / 3.72 / 3.62e8 frames/s)
     int F = (work >= 2048LL * 4 * 48) ? 48 : (work >= 2048LL * 4 * 32) ? 32 : (work >= 1024LL * 4 * 16) ? 16 : 8;
+    // a frame at L >= 1024 is twice the work: runs of 32 (measured on the config-4 slice,
+    // 1024 channels x 861 frames: F = 24 / 32 / 40 / 48 / 64 -> 1.51-1.52 / 1.53-1.54 /
+    // 1.47-1.48 / 1.49-1.50 / 1.46-1.49e8 frames/s)
+    if (h->L_syn >= 1024 && F > 32) F = 32;
     // tuning override (even, 8..256): PV_RUN_FRAMES
     if (const char* ev = std::getenv("PV_RUN_FRAMES")) {
         const int f = std::atoi(ev);
