@@ -208,6 +208,16 @@ struct SynLds {
 struct NoHook {
     __device__ void operator()() const {}
 };
+// where the inverse real-FFT pre-step takes its split twiddles from: LDS, or the caller's
+// registers (v[q] = twiddle of bin lane + 64 q, loaded once per run)
+struct NoTwReg {
+    static constexpr bool ON = false;
+};
+template <int E>
+struct TwReg {
+    static constexpr bool ON = true;
+    float2 v[E];
+};
 // hook(): called once the spectrum row sv has been consumed (before the inverse real-FFT
 // pre-step) — the batched kernel issues the next row's loads there into the same registers.
 // Q1: the output-phase denominator is q = 1 (integer ratio, e.g. pitch 2.0): the unwrap
@@ -215,7 +225,7 @@ struct NoHook {
 // unwrap state is neither read nor updated; phc = fma(rho / 2 pi, phi, +0) is bit for bit
 // what the RACC path computes with q = 1 (R = tj = +0).
 template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false,
-          bool Q1 = false, typename Hook = NoHook>
+          bool Q1 = false, typename Hook = NoHook, typename TwS = NoTwReg>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
@@ -223,7 +233,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                                             float2* tile, int lane, float2 (&z)[Geo<L>::E],
                                             const float (&ekr)[Geo<L>::E + 1],
                                             const unsigned (&jkr)[Geo<L>::E + 1],
-                                            const Hook& hook = Hook{}) {
+                                            const Hook& hook = Hook{}, const TwS& twr = TwS{}) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int B = L + 1;
@@ -365,7 +375,9 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     for (int q = 0; q < E; ++q) {
         const float2 A = Yr[q];
         const float2 Bc = (lane == 0) ? Yr[E - q] : Bp[q];
-        const float2 tw = lds_ld(&twsl[lane + 64 * q]);   // e^{-2 pi i k/N}, k = lane + 64 q
+        float2 tw;  // e^{-2 pi i k/N}, k = lane + 64 q
+        if constexpr (TwS::ON) tw = twr.v[q];
+        else tw = lds_ld(&twsl[lane + 64 * q]);
 #if PV_PK_PRESTEP
         // V = (dr, di) = (A.x - B.x, A.y + B.y), W = (fer, fei) = (A.x + B.x, A.y - B.y):
         // one v_pk_add each, the sign flips by neg_lo / neg_hi;

@@ -23,6 +23,9 @@
                        // synthesis lowers the chip's clock for both), step +1.1 %
                        // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
 #endif
+#ifndef PV_SYN_TWREG
+#define PV_SYN_TWREG 1  // L = 1024 synthesis: split twiddles in registers (syn_run)
+#endif
 #ifndef PV_SYN_KREG
 #define PV_SYN_KREG 0  // measured: no gain over the LDS reads
 #endif
@@ -210,14 +213,24 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
                         (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};
+    // L = 1024: the pre-step's split twiddles of the lane's bins in registers for the run
+    // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy)
+    using TwS = typename std::conditional<(L == 1024 && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
+    TwS twr;
+    if constexpr (TwS::ON) {
+#pragma unroll
+        for (int q = 0; q < E; ++q) twr.v[q] = lds_ld(&sc.twsl[lane + 64 * q]);
+    }
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, NoHook, TwS>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile,
+                                                                           lane, z, ekr, jkr, NoHook{}, twr);
     };
     [[maybe_unused]] auto synth_h = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hook) {
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook);
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, std::decay_t<decltype(hook)>, TwS>(
+            sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook, twr);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
