@@ -308,7 +308,7 @@ hipError_t launch_window_gain(const float* win, float* dwin, float* gain, int n,
 template <int L>
 static size_t syn_lds(int dt) {
     const int ring_floats = (dt > 0) ? 0 : 4 * 2 * L;               // ROLA: tails alias the tiles
-    const int gain_floats = (PV_SYN_GREG && dt > 0 && L <= 512) ? 0 : 2 * L;  // GREG: gains in registers
+    const int gain_floats = (PV_SYN_GREG && dt > 0 && (L <= 512 || (L == 1024 && dt == 4 && PV_SYN_GREG1024))) ? 0 : 2 * L;  // GREG
     return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) +
            sizeof(float) * (ring_floats + gain_floats) + sizeof(float) * 4 * (L + 1 + 3);
 }

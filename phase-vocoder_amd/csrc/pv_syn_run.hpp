@@ -23,6 +23,10 @@
                        // synthesis lowers the chip's clock for both), step +1.1 %
                        // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
 #endif
+#ifndef PV_SYN_GREG1024
+#define PV_SYN_GREG1024 1  // ... and at L = 1024 with out hop 512 (config 4: 252 VGPRs, free below
+                           // the 2 waves/SIMD LDS sets; smaller out hops would need AGPRs)
+#endif
 #ifndef PV_SYN_TWREG
 #define PV_SYN_TWREG 1  // L = 1024 synthesis: split twiddles in registers (syn_run)
 #endif
@@ -142,7 +146,7 @@ struct SynTraits {
     static constexpr int E = Geo<L>::E;
     static constexpr int NS = ROLA ? E : 1;  // register overlap-add slots
     static constexpr int D = ROLA ? DT : 1;  // slots completed per frame (ROLA)
-    static constexpr bool GREG = PV_SYN_GREG && ROLA && L <= 512;
+    static constexpr bool GREG = PV_SYN_GREG && ROLA && (L <= 512 || (L == 1024 && DT == 4 && PV_SYN_GREG1024));
     static constexpr bool RACC = QPOW2 && MODE != 1 && PV_REV_ACC;  // host: QPOW2 only for q <= 4096
 };
 
