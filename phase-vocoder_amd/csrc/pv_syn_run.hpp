@@ -30,6 +30,9 @@
 #ifndef PV_SYN_TWREG
 #define PV_SYN_TWREG 1  // L = 1024 synthesis: split twiddles in registers (syn_run)
 #endif
+#ifndef PV_SYN_TWREG512
+#define PV_SYN_TWREG512 1  // ... and at L = 512 (config 3), within its 3 waves/SIMD budget
+#endif
 #ifndef PV_SYN_KREG
 #define PV_SYN_KREG 0  // measured: no gain over the LDS reads
 #endif
@@ -219,7 +222,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};
     // L = 1024: the pre-step's split twiddles of the lane's bins in registers for the run
     // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy)
-    using TwS = typename std::conditional<(L == 1024 && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
+    using TwS = typename std::conditional<((L == 1024 || (L == 512 && PV_SYN_TWREG512 && LANEK && !HEADSC1)) && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
     TwS twr;
     if constexpr (TwS::ON) {
 #pragma unroll
