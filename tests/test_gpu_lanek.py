@@ -19,7 +19,9 @@ def pv_frames(n, hop):
 
 CASES = [  # (N, hop_div, effect, scale, lane constants expected)
     (1024, 4, TIME_SHIFT, 0.5, 1),     # config 3: q = 2
-    (2048, 4, PITCH_SHIFT, 1.5, 1),    # config 4: q = 2, L = 1024
+    (2048, 4, PITCH_SHIFT, 1.5, 1),    # config 4: q = 2, L = 1024 (gains + split twiddles in registers)
+    (2048, 4, TIME_SHIFT, 0.25, 1),    # L = 1024, out hop 128 (DT = 1), q = 4
+    (2048, 16, PITCH_SHIFT, 1.5, 1),   # L = 1024, hop 128 (DT = 1), q = 2
     (1024, 4, PITCH_SHIFT, 1.25, 1),   # q = 4 divides 64 / 4
     (512, 4, PITCH_SHIFT, 0.75, 1),    # L = 256, hop 128, q = 4 divides 16
     (512, 8, PITCH_SHIFT, 0.75, 0),    # out hop 64: the LDS-ring synthesis reads the tables
