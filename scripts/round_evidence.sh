@@ -23,7 +23,7 @@ for s in $STEPS; do
     rt) run bench_rt 300 python bench.py --workload rt ;;
     prof)
       rm -rf gpurun_out/prof
-      run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu ;;
+      run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 40 --warmup 3 --no-cpu ;;
     pmc)
       rm -rf gpurun_out/pmc
       PMC_SETS=scripts/pmc_sets_r1.txt PROF_ARGS="--calib" timeout -k 10 900 bash scripts/pmc_session.sh > gpurun_out/pmc_session.log 2>&1
