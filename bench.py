@@ -11,6 +11,10 @@ ranks with no data-path collective (weak scaling).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--no-cpu]
   torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL)
 
+`--gpus N` without a launcher starts the N rank processes itself (launch_ranks); with one
+(WORLD_SIZE set) it must equal WORLD_SIZE.  PV_DIST_BACKEND=gloo runs the same N-rank path
+over gloo (collectives on host tensors) — how the one-GPU box rehearses it.
+
 The synthetic channels are generated once on the host and uploaded; after the timed
 steps the whole output is checked for finiteness and 16 channels spread over the batch
 (first and last included) are compared with the CPU oracle (`rms_vs_oracle`, bar 1e-5
@@ -151,12 +155,23 @@ def main():
                          "single 60 s stream, pitch 2.0; c4: configs[3] per-GPU slice (1024 ch, "
                          "N=2048 hop=512, pitch 1.5); rt: configs[4] real-time mode")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                             "(one rank per GPU: the two must agree)")
+    elif args.gpus > 1:
+        # no launcher: start one rank process per GPU here, before anything touches the GPU
+        return launch_ranks(args.gpus)
     # a c2 step is ~50 us: 10 steps would time the barrier/synchronise bracket, not the path
     if args.steps is None:
         args.steps = 200 if args.workload == "c2" else 10
     if args.warmup is None:
         args.warmup = 20 if args.workload == "c2" else 3
     if args.workload == "rt":
+        if args.gpus > 1:
+            raise SystemExit("bench.py: the real-time workload runs on one GPU (--gpus 1)")
         return bench_rt(args)
 
     import torch
@@ -164,11 +179,19 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs (the one-GPU rehearsal of the N-rank path,
+    # PV_DIST_BACKEND=gloo) share the devices round-robin
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    backend = os.environ.get("PV_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on ROCm
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
+    # the device the few collectives of the bench (timing, check) run on
+    cdev = dev if backend == "nccl" else torch.device("cpu")
 
     from pvamd import PITCH_SHIFT, PhaseVocoder, STANDARD, TIME_SHIFT
 
@@ -223,7 +246,7 @@ def main():
     prof = pv.profile_read()
     pv.profile(False)
 
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
@@ -236,10 +259,7 @@ def main():
                  "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
                  "carry": 0, "runsum": 8 * B, "seam": 0,
                  # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
-                 "fused": 4 * hop_a + 8 * B + 4 * hop_s,
-                 # q = 2^e single launch chained over run groups (pv_chain.hip): the spectrum is
-                 # written once (an output) and re-read from L2 / MALL, not counted twice
-                 "chain": 4 * hop_a + 8 * B + 4 * hop_s}
+                 "fused": 4 * hop_a + 8 * B + 4 * hop_s}
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     avg_ms = ms_tot / max(launches, 1)
@@ -284,7 +304,7 @@ def main():
                              frames, finite)
         if world > 1:  # worst rank
             t = torch.tensor([check["max"], check["mean"], 0.0 if check["pass"] else 1.0,
-                              0.0 if finite else 1.0], dtype=torch.float64, device=dev)
+                              0.0 if finite else 1.0], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             check.update(max=float(t[0]), mean=float(t[1]), ranks=world,
                          channels=f"{len(idx)} per rank (indices as rank 0's, rank-local)")
@@ -308,7 +328,8 @@ def main():
             "data": "synthetic (3 sines U[55,4000] Hz a=0.1 + U(+-1e-3) noise, seed 20240+ch)",
             "config": {"workload": wl_desc,
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
-                       "out_hop": hop_s, "parallelism": f"channel-shard x{world}"},
+                       "out_hop": hop_s, "parallelism": f"channel-shard x{world}",
+                       "dist_backend": backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
@@ -408,10 +429,43 @@ def bench_rt(args):
     print(json.dumps(line), flush=True)
 
 
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this script
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), as torchrun would.
+    This parent never touches the GPU and never re-execs; it waits for the ranks, stops the
+    others if one fails, and exits with the first failing rank's status (rank 0 prints the
+    JSON line)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def pv_frames(n, hop):
     from pvamd import frame_count
     return frame_count(n, hop)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

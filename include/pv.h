@@ -105,9 +105,7 @@ typedef struct pv_info {
     int mode, effect;
     float scale;
     int single_launch;        /* what pv_process launches: 0 the split path (analysis, scan,
-                                 synthesis, seams), 1 one q = 1 launch (pv_fused.hip), 2 one
-                                 launch chained over run groups (q = 2^e, pv_chain.hip; an
-                                 unaligned input falls back to the split path)            */
+                                 synthesis, seams), 1 one q = 1 launch (pv_fused.hip)      */
     int single_launch_frames; /* frames per run of that launch (0 for the split path)     */
     int lane_constants;       /* 1: the split synthesis keeps the per-bin unwrap constants
                                  in registers (e_k and (p j_k) mod q repeat every 64 bins:
@@ -216,11 +214,6 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
  * out[k] = win[k]^2 * in[k] + (k + hop < N ? back[k + hop] : 0).  Device pointers. */
 pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,
                               int n, int hop, void* stream);
-
-/* Waits for the handle's device and reports a failed in-kernel hand-off of the chained
- * path (a run-group record that never arrived: never expected; the kernel then drains
- * with wrong output instead of hanging) as PV_ERR_HIP; PV_OK otherwise. */
-pv_status pv_check_device(pv_handle* h);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py). */
 pv_status pv_profile_enable(pv_handle* h, int enable);

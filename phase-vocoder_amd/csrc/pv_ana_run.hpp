@@ -1,8 +1,7 @@
 // pv_ana_run.hpp — one wave's STANDARD analysis run (window -> real FFT -> {mag, phase}
-// rows -> unwrap decisions), shared by the split path's K1 (k_std_analysis, pv_analysis.hip)
-// and the single-launch chained path (k_chain, pv_chain.hip).
+// rows -> unwrap decisions) of the split path's K1 (k_std_analysis, pv_analysis.hip).
 //
-// Both translation units are compiled without SLP vectorisation (-fno-slp-vectorize,
+// Its translation unit is compiled without SLP vectorisation (-fno-slp-vectorize,
 // Makefile): the per-bin scalar chains (real split, atan2, unwrap) then stay scalar instead
 // of being paired into v_pk_* operations that need register moves and sign flips to
 // assemble their operands (measured: analysis -6 %).
@@ -60,20 +59,18 @@ struct AnaLds {
     const float* ekl;    // expected advance e_k per bin (EKL) — else e_lane
 };
 
-// One wave = one run of frames t0 .. t0 + nfr - 1 of channel c.
-// HALO: the frame t0 - 1 is transformed too (phase only) to seed phprev, so the run's first
-// decision m0 = m(t0) is known here (split path: it goes to the run record); without HALO
-// (chained path) the first frame's decision is left to the caller, which gets phi(t0) in
-// phfirst.  On return phprev = phi of the run's last frame and sacc = -(sum of the
-// decisions of frames t0 + 1 .. t0 + nfr - 1) as exact small integers in fp32.
-// NT: non-temporal row stores (the split path's rows are read back by another launch, long
-// after they would have left the caches; the chained path re-reads them from L2 / MALL).
-// rec (nullable): the split path's run record {S, m0}.
-template <int L, bool EKL, int D, bool HALO, bool NT>
+// One wave = one run of frames t0 .. t0 + nfr - 1 of channel c.  The frame t0 - 1 (halo)
+// is transformed too (phase only) to seed phprev, so the run's first decision m0 = m(t0)
+// is known here and goes to the run record.  On return phprev = phi of the run's last
+// frame and sacc = -(sum of the decisions of frames t0 + 1 .. t0 + nfr - 1) as exact small
+// integers in fp32.
+// NT: non-temporal row stores (the rows are read back by another launch, long after they
+// would have left the caches).  rec (nullable): the run record {S, m0}.
+template <int L, bool EKL, int D, bool NT>
 __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
                                         float e_lane, int* rec, float (&phprev)[Geo<L>::E + 1],
-                                        float (&sacc)[Geo<L>::E + 1], float (&phfirst)[Geo<L>::E + 1]) {
+                                        float (&sacc)[Geo<L>::E + 1]) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -86,7 +83,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     (void)ekl;
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
-    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0.0f; phfirst[i] = 0.0f; })
+    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0.0f; })
 
     // One frame: window + FFT + split + atan2 (+ spectrum row, decisions) from raw samples.
     // IS_HALO (frame t0 - 1): phase only, it seeds phprev.
@@ -148,6 +145,9 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
 #ifdef PV_ABL_NOSTORE  // timing-only ablation: the stores never execute (p.frames > 0)
                         if (p.frames < 0)
 #endif
+#ifdef PV_TMP_NOBINL
+                        if (i < E)
+#endif
                         __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
                     } else {
                         *reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]) = f2v{mag, ph};
@@ -159,11 +159,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                     sacc[i] += mr;
                     if (u == 0) {
                         sacc[i] -= mr;
-                        if constexpr (HALO) {
-                            if (rec != nullptr && (i < E || lane == 0)) rec[BP + k] = -(int)mr;
-                        } else {
-                            phfirst[i] = ph;
-                        }
+                        if (rec != nullptr && (i < E || lane == 0)) rec[BP + k] = -(int)mr;
                     }
                 }
                 phprev[i] = ph;
@@ -190,7 +186,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     // last frame fully inside: floor((n - N) / hop), -1 when n < N (C++ division truncates
     // toward zero, which for N - hop < n < N would give 0 and read frame 0 past the end)
     const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
-    if (HALO && t0 > 0) {
+    if (t0 > 0) {
         float2 xh[E], z[E];
         if (t0 - 1 <= lastfull) load_fast(-1, xh); else load_checked(-1, xh);
         window(xh, z);

@@ -1,8 +1,7 @@
 // pv_analysis.hip — K1, the analysis kernels (STANDARD and REF_COMPAT), gfx950.
 //
-// Its own translation unit, compiled without SLP vectorisation (pv_ana_run.hpp, which
-// holds the per-run body shared with the chained path; the synthesis, whose packed code
-// is hand-written, is faster with SLP on).
+// Its own translation unit, compiled without SLP vectorisation (the per-run body is in
+// pv_ana_run.hpp; the synthesis, whose packed code is hand-written, is faster with SLP on).
 // Pipeline and geometry: pv_kernels.hip header, DESIGN.md §4.
 #include "pv_ana_run.hpp"
 
@@ -60,9 +59,9 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     // run record {S, m0}: m0 (the decision of the run's first frame) is stored as soon as
     // it is known, S after the loop
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * 2 * p.bins_pad : nullptr;
-    float phprev[E + 1], sacc[E + 1], phfirst[E + 1];
-    ana_run<L, EKL, D, true, (bool)PV_NT_SPEC>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c,
-                                              t0, nfr, e_lane, rec, phprev, sacc, phfirst);
+    float phprev[E + 1], sacc[E + 1];
+    ana_run<L, EKL, D, (bool)PV_NT_SPEC>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c,
+                                        t0, nfr, e_lane, rec, phprev, sacc);
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT

@@ -38,10 +38,10 @@ pv_status fail(pv_status s, const std::string& msg) {
     } while (0)
 
 constexpr double kPi = 3.14159265358979323846;
-constexpr int kNumKernels = 9;
+constexpr int kNumKernels = 8;
 const char* kKernelNames[kNumKernels] = {"analysis", "runsum", "carry", "synthesis",
-                                         "seam", "compat_analysis", "rt", "fused", "chain"};
-enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5, KRT = 6, KF = 7, KCH = 8 };
+                                         "seam", "compat_analysis", "rt", "fused"};
+enum { KA = 0, KRS = 1, KC = 2, KS = 3, KSEAM = 4, KCA = 5, KRT = 6, KF = 7 };
 
 bool is_pow2(long long v) { return v > 0 && (v & (v - 1)) == 0; }
 
@@ -102,8 +102,6 @@ struct pv_handle {
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
-    int F_chain = 0;  // frames per run of the single-launch chained q = 2^e path (0: not available)
-    unsigned chain_epoch = 0;  // launch tag of the chained path's run-group records
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
@@ -117,9 +115,7 @@ struct pv_handle {
     // workspace
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
-    int* d_seam_flags = nullptr;  // fused/chained paths: per (channel, workgroup) arrival counters
-    unsigned *d_chain_ticket = nullptr, *d_chain_flags = nullptr;  // chained path (pv_chain.hip)
-    int *d_chain_rec = nullptr, *d_chain_err = nullptr;
+    int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
     unsigned long long* d_clk = nullptr;  // PV_CLOCK_PROBE builds only
     Profile prof;
 };
@@ -360,88 +356,6 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     return PV_OK;
 }
 
-// q = 2^e > 1 (STANDARD): analysis, the unwrap scan, resynthesis and every seam in one
-// launch chained over run groups (pv_chain.hip); outputs equal to do_analysis +
-// do_resynthesis bit for bit at equal F.  Needs 8-byte aligned input (the shifted-register
-// analysis); returns PV_ERR_UNSUPPORTED otherwise so the caller takes the split path.
-pv_status do_chain(pv_handle* h, const float* x, long long ldx, long long n, int C, int frames,
-                   pv_float2* spec, long long ld_spec, float* out, long long ldo, hipStream_t s) {
-    if (C == 0 || frames == 0) return PV_OK;
-    if (!x || !spec || !out) return fail(PV_ERR_ARG, "null x/spec/out");
-    if (ld_spec < (long long)frames * h->spec_stride)
-        return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
-    if (C > 1 && ldx < n) return fail(PV_ERR_ARG, "ldx < n_samples");
-    const long long olen = pv_output_length(h, frames);
-    if (C > 1 && ldo < olen) return fail(PV_ERR_ARG, "ldo < pv_output_length");
-    const bool aligned = (((uintptr_t)x & 7) == 0) && (ldx % 2 == 0);
-    if (!aligned) return PV_ERR_UNSUPPORTED;
-    const int F = h->F_chain;
-    const int nruns = (frames + F - 1) / F;
-    pv::ChainParams p{};
-    pv::AnaParams& a = p.a;
-    a.x = x;
-    a.ldx = ldx;
-    a.n = n;
-    a.hop = h->hop;
-    a.frames = frames;
-    a.F = F;
-    a.nruns = nruns;
-    a.aligned = 1;
-    a.win = h->d_win;
-    a.tw = h->d_tw_syn;    // the stage-major L-point table serves both directions
-    a.tws = h->d_tws_syn;  // e^{-2 pi i k/N}, k <= N/2: the analysis split's table too
-    a.ek = h->d_ek;
-    a.ek_lane = 1;
-    a.spec = reinterpret_cast<float2*>(spec);
-    a.ld_spec = ld_spec;
-    a.spec_stride = h->spec_stride;
-    a.runsum = nullptr;
-    a.bins_pad = h->bins_pad;
-    a.clk = nullptr;
-    pv::SynParams& y = p.s;
-    y.spec = reinterpret_cast<const float2*>(spec);
-    y.ld_spec = ld_spec;
-    y.spec_stride = h->spec_stride;
-    y.frames = frames;
-    y.F = F;
-    y.nruns = nruns;
-    y.bins_pad = h->bins_pad;
-    y.carry = nullptr;
-    y.ek = h->d_ek;
-    y.jk_mod = h->d_jk_mod;
-    y.src_first = h->d_src_first;
-    y.src_cnt = h->d_src_cnt;
-    y.pitch = h->pitch;
-    y.rho = h->rho;
-    y.p_mod = h->p_mod;
-    y.q = h->q;
-    y.q_pow2 = h->q_pow2;
-    y.inv_q = h->inv_q;
-    y.tw = h->d_tw_syn;
-    y.tws = h->d_tws_syn;
-    y.gain = h->d_gain;
-    y.rot = 0;
-    y.hs = h->hs;
-    y.out = out;
-    y.ldo = ldo;
-    y.out_len = olen;
-    y.out_aligned = ((reinterpret_cast<uintptr_t>(out) & 7) == 0) && ((ldo & 1) == 0);
-    y.tails = h->d_tails;
-    y.tail_len = h->tail_len;
-    p.channels = C;
-    p.nwg = (nruns + 3) / 4;
-    if (++h->chain_epoch == 0) h->chain_epoch = 1;  // flags start at 0: never a valid tag
-    p.epoch = h->chain_epoch;
-    p.ticket = h->d_chain_ticket;
-    p.flags = h->d_chain_flags;
-    p.rec = h->d_chain_rec;
-    p.seam_flags = h->d_seam_flags;
-    p.err = h->d_chain_err;
-    PV_HIP(hipMemsetAsync(h->d_chain_ticket, 0, sizeof(unsigned), s));
-    PV_LAUNCH(h, KCH, s, pv::launch_chain(h->L_syn, h->pitch ? 2 : 0, p, s));
-    return PV_OK;
-}
-
 }  // namespace
 
 extern "C" {
@@ -485,8 +399,8 @@ pv_status pv_get_info(const pv_handle* h, pv_info* info) {
     info->mode = h->mode;
     info->effect = h->effect;
     info->scale = h->scale;
-    info->single_launch = h->F_fused > 0 ? 1 : h->F_chain > 0 ? 2 : 0;
-    info->single_launch_frames = h->F_fused > 0 ? h->F_fused : h->F_chain;
+    info->single_launch = h->F_fused > 0 ? 1 : 0;
+    info->single_launch_frames = h->F_fused;
     info->lane_constants = h->k_lane;
     return PV_OK;
 }
@@ -496,8 +410,7 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_clk, h->d_chain_ticket,
-                    h->d_chain_flags, h->d_chain_rec, h->d_chain_err};
+                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_clk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
@@ -710,43 +623,18 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     }
     const int runs_fused = h->F_fused > 0 ? (cfg->max_frames + h->F_fused - 1) / h->F_fused : 0;
 
-    // ---- single-launch chained path (q = 2^e <= 4096, pv_chain.hip): opt-in with PV_CHAIN=1
-    // (measured slower than the split path on config 3, pv_chain.hip header);
-    // PV_CHAIN_FRAMES overrides its run length
-    const char* chain_env = std::getenv("PV_CHAIN");
-    if (chain_env && chain_env[0] == '1' && h->mode == PV_MODE_STANDARD && h->q > 1 && h->q_pow2 &&
-        h->q <= 4096 && pv::chain_supported(h->L_syn, h->hs, h->hop, cfg->hop_div)) {
-        int Fc = 48;
-        if (const char* ev = std::getenv("PV_CHAIN_FRAMES")) {
-            const int f = std::atoi(ev);
-            if (f >= 2 && f <= 256 && f % 2 == 0) Fc = f;
-        }
-        while ((long long)Fc * h->hs < h->tail_len) Fc += 2;
-        h->F_chain = Fc;
-    }
-    const int runs_chain = h->F_chain > 0 ? (cfg->max_frames + h->F_chain - 1) / h->F_chain : 0;
-
     // ---- workspace
     const size_t chans = (size_t)std::max(cfg->max_channels, 1);
     const size_t runs_total = chans * std::max(h->max_runs, 1);
-    const size_t wg_total = chans * std::max((std::max(std::max(h->max_runs, runs_fused), runs_chain) + 3) / 4, 1);
+    const size_t wg_total = chans * std::max((std::max(h->max_runs, runs_fused) + 3) / 4, 1);
     if (h->mode == PV_MODE_STANDARD) {
         PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * 2 * h->bins_pad));
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
     }
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
-    if (h->F_fused > 0 || h->F_chain > 0) {
+    if (h->F_fused > 0) {
         PV_HIP(hipMalloc((void**)&h->d_seam_flags, sizeof(int) * wg_total));
         PV_HIP(hipMemset(h->d_seam_flags, 0, sizeof(int) * wg_total));
-    }
-    if (h->F_chain > 0) {
-        const size_t groups = chans * std::max((runs_chain + 3) / 4, 1);
-        PV_HIP(hipMalloc((void**)&h->d_chain_rec, sizeof(int) * groups * 2 * h->bins_pad));
-        PV_HIP(hipMalloc((void**)&h->d_chain_flags, sizeof(unsigned) * groups));
-        PV_HIP(hipMemset(h->d_chain_flags, 0, sizeof(unsigned) * groups));
-        PV_HIP(hipMalloc((void**)&h->d_chain_ticket, sizeof(unsigned)));
-        PV_HIP(hipMalloc((void**)&h->d_chain_err, sizeof(int)));
-        PV_HIP(hipMemset(h->d_chain_err, 0, sizeof(int)));
     }
 #ifdef PV_CLOCK_PROBE
     PV_HIP(hipMalloc((void**)&h->d_clk, sizeof(unsigned long long) * 2 * runs_total));
@@ -787,10 +675,6 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     DeviceGuard g(h->cfg.device);
     hipStream_t s = (hipStream_t)stream;
     if (h->F_fused > 0) return do_fused(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
-    if (h->F_chain > 0) {
-        st = do_chain(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
-        if (st != PV_ERR_UNSUPPORTED) return st;  // unaligned input: the split path below
-    }
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
     if (st != PV_OK) return st;
@@ -916,21 +800,6 @@ pv_status pv_test_overlap_add(const float* in, const float* win, const float* ba
     if (!in || !win || !back || !out || n <= 0 || hop < 0) return fail(PV_ERR_ARG, "bad argument");
     hipError_t e = pv::launch_overlap_test(in, win, back, out, n, hop, (hipStream_t)stream);
     if (e != hipSuccess) return fail(PV_ERR_HIP, std::string("test_overlap_add: ") + hipGetErrorString(e));
-    return PV_OK;
-}
-
-pv_status pv_check_device(pv_handle* h) {
-    if (!h) return fail(PV_ERR_ARG, "null handle");
-    DeviceGuard g(h->cfg.device);
-    PV_HIP(hipDeviceSynchronize());
-    if (h->d_chain_err) {
-        int err = 0;
-        PV_HIP(hipMemcpy(&err, h->d_chain_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (err) {
-            PV_HIP(hipMemset(h->d_chain_err, 0, sizeof(int)));  // reported once
-            return fail(PV_ERR_HIP, "chained path: a run-group record never arrived (output invalid)");
-        }
-    }
     return PV_OK;
 }
 

@@ -85,20 +85,6 @@ struct FusedParams {
     int* seam_flags;                   // [C][nwg] arrival counters, 0 between launches
 };
 
-// single-launch STANDARD path for q = 2^e > 1, chained over run groups (pv_chain.hip)
-struct ChainParams {
-    AnaParams a;                       // input, spectrum, analysis tables (a.runsum unused)
-    SynParams s;                       // spectrum, output, synthesis tables, tails (s.carry unused)
-    int channels, nwg;                 // workgroups per channel = ceil(nruns / 4)
-    unsigned epoch;                    // launch tag of the run-group records (never 0)
-    unsigned* ticket;                  // workgroup ticket counter, 0 at launch
-    unsigned* flags;                   // [nwg][channels] epoch of the published record
-    int* rec;                          // [nwg][channels][2][bins_pad] {count through the group's
-                                       //   last frame, that frame's phases}
-    int* seam_flags;                   // [channels][nwg] arrival counters, 0 between launches
-    int* err;                          // set when a wait timed out (never expected)
-};
-
 struct SeamParams {
     float* out;
     long long ldo, out_len;
@@ -160,9 +146,6 @@ hipError_t launch_seam(int channels, const SeamParams& p, hipStream_t s);
 bool fused_supported(int L, int hs);
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s);
 size_t synthesis_lds_bytes(int L, int hs);
-bool chain_supported(int L, int hs, int hop, int hop_div);
-size_t chain_lds_bytes(int L);
-hipError_t launch_chain(int L, int mode, const ChainParams& p, hipStream_t s);
 hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
                       hipStream_t s);
 hipError_t launch_mix(const MixParams& p, hipStream_t s);

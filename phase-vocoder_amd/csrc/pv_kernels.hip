@@ -198,8 +198,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     }
     constexpr int NS = SynTraits<L, MODE, DT, QPOW2>::NS, D = SynTraits<L, MODE, DT, QPOW2>::D;
     float2 acc[NS];
-    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, false, LANEK>(
-        p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, false, M, phprev, acc);
+    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, LANEK>(
+        p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, M, phprev, acc);
     if constexpr (ROLA) {
         // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
         __syncthreads();

@@ -1,7 +1,7 @@
 // pv_syn_run.hpp — one wave's synthesis run (phase propagation -> polar->rect -> inverse
-// real FFT -> window -> overlap-add -> final samples to `out`), shared by the split path's
-// K3 (k_synthesis, pv_kernels.hip) and the single-launch chained path (k_chain,
-// pv_chain.hip).  Geometry and overlap-add: pv_kernels.hip, K3.
+// real FFT -> window -> overlap-add -> final samples to `out`) of the split path's K3
+// (k_synthesis, pv_kernels.hip), and the in-launch seam hand-off of the single-launch q = 1
+// path (pv_fused.hip).  Geometry and overlap-add: pv_kernels.hip, K3.
 #pragma once
 #include "pv_frame.hpp"
 #include "pv_kernels.h"
@@ -39,8 +39,8 @@
 
 namespace pv {
 
-// sc1 (write-through) stores / loads of the inter-workgroup hand-offs (pv_fused.hip,
-// pv_chain.hip; MI355X_MICROARCH.md "Valid forms")
+// sc1 (write-through) stores / loads of the inter-workgroup hand-offs (pv_fused.hip;
+// MI355X_MICROARCH.md "Valid forms")
 __device__ __forceinline__ void st_sc1(float* p, float v) {
     asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
 }
@@ -157,16 +157,14 @@ struct SynTraits {
 // zero), unwrap state M / phprev initialised by the caller (M = the carry at t0, in the RACC
 // form when RACC).  On return acc holds the run's overlap tail (ROLA; slots D..NS-1) or
 // the ring does (DT = 0).
-// NTROW: spectrum rows loaded non-temporally.  HEADSC1: the positions < N - hs of a run
-// whose workgroup has a predecessor (head) are stored write-through (sc1) for an in-kernel
-// seam hand-off; `head` says whether this wave's run is such a head.
+// NTROW: spectrum rows loaded non-temporally.
 // LANEK: the unwrap constants are per-lane (e_k and (p j_k) mod q depend on k mod 64 only:
 // 64 a multiple of the hop divisor and q of 64 / hop divisor, checked by the host —
 // config 3 and 4): two registers (and bin L's j constant) instead of two LDS reads per bin
 // and frame.
-template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool HEADSC1, bool LANEK = false>
+template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool LANEK = false>
 __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, const float2 (&tw0)[Geo<L>::E],
-                                        int lane, int w, int c, int t0, int nfr, bool head,
+                                        int lane, int w, int c, int t0, int nfr,
                                         int (&M)[Geo<L>::E + 1], float (&phprev)[Geo<L>::E + 1],
                                         float2 (&acc)[SynTraits<L, MODE, DT, QPOW2>::NS]) {
     using G_ = Geo<L>;
@@ -181,7 +179,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     constexpr bool RACC = T_::RACC;
     const int hs = p.hs;
     const int TL = N - hs;
-    (void)TL; (void)head;
+    (void)TL;
     float2* tile = sc.tiles + w * G_::TILE;
     float* ring = sc.rings + w * N;
     const float* gainl = sc.gainl;
@@ -222,7 +220,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};
     // L = 1024: the pre-step's split twiddles of the lane's bins in registers for the run
     // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy)
-    using TwS = typename std::conditional<((L == 1024 || (L == 512 && PV_SYN_TWREG512 && LANEK && !HEADSC1)) && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
+    using TwS = typename std::conditional<((L == 1024 || (L == 512 && PV_SYN_TWREG512 && LANEK)) && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
     TwS twr;
     if constexpr (TwS::ON) {
 #pragma unroll
@@ -256,24 +254,15 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     auto flush_regs = [&](int u, auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
         const long long pb = obase + (long long)u * hs + 2 * lane;
-        // head positions of a chained workgroup go out write-through (wave-uniform)
-        const bool hd = HEADSC1 && head && (u * hs < TL);
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const long long gp = pb + 128 * d;
             if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
-                if (HEADSC1 && hd) {
-                    st_sc1(outc + gp, f2v{acc[d].x, acc[d].y});
-                } else {
 #if PV_NT_OUT
-                    __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
+                __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
 #else
-                    *reinterpret_cast<float2*>(outc + gp) = acc[d];
+                *reinterpret_cast<float2*>(outc + gp) = acc[d];
 #endif
-                }
-            } else if (HEADSC1 && hd) {
-                if (gp < p.out_len) st_sc1(outc + gp, acc[d].x);
-                if (gp + 1 < p.out_len) st_sc1(outc + gp + 1, acc[d].y);
             } else {
                 if (gp < p.out_len) outc[gp] = acc[d].x;
                 if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;

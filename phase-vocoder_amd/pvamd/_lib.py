@@ -85,9 +85,6 @@ def lib():
     L.pv_set_window.restype = i
     L.pv_test_overlap_add.argtypes = [vp, vp, vp, vp, i, i, vp]
     L.pv_test_overlap_add.restype = i
-    if hasattr(L, "pv_check_device"):  # (A/B builds of older revisions lack it)
-        L.pv_check_device.argtypes = [vp]
-        L.pv_check_device.restype = i
     L.pv_profile_enable.argtypes = [vp, i]
     L.pv_profile_enable.restype = i
     L.pv_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),

@@ -72,7 +72,7 @@ class PhaseVocoder:
         self.spec_bins = info.spec_bins
         self.spec_stride = info.spec_stride
         self.frames_per_run = info.frames_per_run
-        # 0 split path, 1 single q = 1 launch, 2 single launch chained over run groups
+        # 0 split path, 1 single q = 1 launch (pv_fused.hip)
         self.single_launch = info.single_launch
         self.single_launch_frames = info.single_launch_frames
         self.lane_constants = info.lane_constants
@@ -228,10 +228,6 @@ class PhaseVocoder:
                    "pv_import_tables")
 
     # -------------------------------------------------------------- profiling (bench.py)
-    def check_device(self):
-        """Wait for the device; raises if a chained launch's hand-off timed out."""
-        self._call(self._L.pv_check_device(self._h), "pv_check_device")
-
     def profile(self, enable: bool = True):
         self._call(self._L.pv_profile_enable(self._h, 1 if enable else 0), "pv_profile_enable")
 

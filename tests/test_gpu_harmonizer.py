@@ -37,10 +37,8 @@ def test_harmonizer_voices_and_mix(cuda, monkeypatch, N, ratios):
     voices, mix, _ = hz.harmonize(torch.from_numpy(xs).cuda(), gains=gains)
     v = voices.cpu().numpy()
     # the voices run the split path; a single pv_process would take the fused (integer ratio)
-    # or the chained (ratio p/2^e) launch with its own run length (same values up to the
-    # seams, tests/test_gpu_fused.py, tests/test_gpu_chain.py)
+    # launch with its own run length (same values up to the seams, tests/test_gpu_fused.py)
     monkeypatch.setenv("PV_FUSED", "0")
-    monkeypatch.setenv("PV_CHAIN", "0")
     for k, r in enumerate(ratios):
         pv = PhaseVocoder(N, PITCH_SHIFT, r, 4, mode=STANDARD, max_channels=C, max_frames=400)
         single, _ = pv.process(torch.from_numpy(xs).cuda())

@@ -242,7 +242,6 @@ def test_run_length_geometries(cuda, monkeypatch, F, effect, scale):
     the oracle's output; run boundaries only move the seams (<= 1e-6 between runs)."""
     N, hop_div, C = 1024, 4, 3
     xs = np.stack([synth(110250, 20240 + c) for c in range(C)])
-    monkeypatch.setenv("PV_CHAIN", "0")  # the split path's geometries (the chained one: test_gpu_chain.py)
     monkeypatch.setenv("PV_RUN_FRAMES", str(F))
     pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=440)
     assert pv.frames_per_run == F
