@@ -150,6 +150,10 @@ def main():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the timed batch (profiling passes only)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--layout", choices=["packed", "natural"], default="packed",
+                    help="STANDARD spectrum rows of the pv_process workspace (include/pv.h "
+                         "pv_spec_layout): packed (default) folds the real bin N/2 into slot 0 "
+                         "so every row store is whole 64-byte segments")
     ap.add_argument("--workload", choices=["c3", "c2", "c4", "rt", "batch"], default="c3",
                     help="c3 (= batch): configs[2], the headline line (default); c2: configs[1] "
                          "single 60 s stream, pitch 2.0; c4: configs[3] per-GPU slice (1024 ch, "
@@ -194,6 +198,7 @@ def main():
     cdev = dev if backend == "nccl" else torch.device("cpu")
 
     from pvamd import PITCH_SHIFT, PhaseVocoder, STANDARD, TIME_SHIFT
+    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED
 
     wl = "c3" if args.workload == "batch" else args.workload
     # (N, hop_div, effect, scale, seconds, channels per GPU, description)
@@ -208,8 +213,9 @@ def main():
                  "PV_STANDARD pitch 1.5 (8192 ch on 8 GPUs)")}
     N, hop_div, effect, scale, seconds, C, wl_desc = WL[wl]
     n = int(round(seconds * SR))
+    layout = PV_SPEC_PACKED if args.layout == "packed" else PV_SPEC_NATURAL
     pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C,
-                      max_frames=pv_frames(n, N // hop_div), device=local)
+                      max_frames=pv_frames(n, N // hop_div), device=local, spec_layout=layout)
     frames = pv.num_frames(n)
     tables = None
     if world > 1:  # init-time RCCL broadcast of rank 0's tables (north_star); not timed
@@ -253,8 +259,10 @@ def main():
     total_frames = C * frames * world * args.steps
     value = total_frames / dt
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time
-    hop_a, hop_s, B = N // hop_div, pv.outHopSize, N // 2 + 1
+    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
+    # Spectrum bytes per frame = the row the layout stores: 8 (N/2+1) natural,
+    # 8 N/2 packed (bin N/2 rides in slot 0): the packed figure is the smaller, not inflated
+    hop_a, hop_s, B = N // hop_div, pv.outHopSize, pv.spec_bins
     per_frame = {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
                  "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
                  "carry": 0, "runsum": 8 * B, "seam": 0,
@@ -270,29 +278,31 @@ def main():
         try:
             tj = json.load(open(args.traffic))
             # measured on one workload (config 3 by default): no number for the others
-            if tj.get("_workload", "c3") == wl:
+            if tj.get("_workload", "c3") == wl and tj.get("_layout", "natural") == args.layout:
                 traffic = tj.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
-    # the box's measured HBM ceilings (scripts/bw_probe.hip -> profiles/r02_bw_probe.jsonl,
-    # random data, several accesses in flight per lane): the 8 TB/s peak is the spec figure;
-    # plain streams reach ~6 TB/s, and the analysis kernel's own byte mix and store shape
-    # with no arithmetic at all (ana_mix_nt) runs at ~4.8 TB/s on MI355X
+    # the box's measured HBM ceilings: plain streams (scripts/bw_probe.hip ->
+    # profiles/r02_bw_probe.jsonl: copy ~6.0, write ~6.0 TB/s against the 8 TB/s spec) and the
+    # dominant kernel's own byte mix with no arithmetic, in the product's wave mapping and row
+    # layout (scripts/layout_probe.hip -> profiles/r03_layout_probe.jsonl, config 3 only)
     ceiling = None
-    probe = os.path.join(ROOT, "profiles", "r02_bw_probe.jsonl")
-    if os.path.exists(probe):
-        try:
-            rows = {d["probe"]: d["GBps"] for d in map(json.loads, open(probe)) if d}
-            copy = max(v for k, v in rows.items() if k.startswith("copy"))
-            write = max(v for k, v in rows.items() if k.startswith("write"))
-            ceiling = {"copy_GBps": copy, "write_GBps": write, "frac_of_copy": achieved / copy,
-                       "traffic_frac_of_copy": (traffic / (avg_ms * 1e-3) / 1e9 / copy) if traffic else None,
-                       "source": "profiles/r02_bw_probe.jsonl"}
-            pat = {"analysis": "ana_mix_nt", "synthesis": "syn_mix"}.get(dom)
-            if pat in rows and wl == "c3":
-                ceiling.update(pattern=pat, pattern_GBps=rows[pat], frac_of_pattern=achieved / rows[pat])
-        except Exception:
-            ceiling = None
+    try:
+        rows = {}
+        for f in ("r02_bw_probe.jsonl", "r03_layout_probe.jsonl"):
+            for d in map(json.loads, open(os.path.join(ROOT, "profiles", f))):
+                rows.setdefault(d["probe"], d["GBps"])
+        copy = max(v for k, v in rows.items() if k.startswith("copy"))
+        write = max(v for k, v in rows.items() if k.startswith("write"))
+        ceiling = {"copy_GBps": copy, "write_GBps": write, "frac_of_copy": achieved / copy,
+                   "traffic_frac_of_copy": (traffic / (avg_ms * 1e-3) / 1e9 / copy) if traffic else None,
+                   "source": "profiles/r02_bw_probe.jsonl, profiles/r03_layout_probe.jsonl"}
+        suffix = "512" if args.layout == "packed" else "520_L"
+        pat = {"analysis": f"ana_cmaj_product_{suffix}", "synthesis": f"syn_cmaj_product_{suffix}"}.get(dom)
+        if pat in rows and wl == "c3":
+            ceiling.update(pattern=pat, pattern_GBps=rows[pat], frac_of_pattern=achieved / rows[pat])
+    except Exception:
+        ceiling = None
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}
 
     # parity of the timed batch: every sample finite, sampled channels vs the oracle
@@ -328,7 +338,8 @@ def main():
             "data": "synthetic (3 sines U[55,4000] Hz a=0.1 + U(+-1e-3) noise, seed 20240+ch)",
             "config": {"workload": wl_desc,
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
-                       "out_hop": hop_s, "parallelism": f"channel-shard x{world}",
+                       "out_hop": hop_s, "spec_layout": args.layout,
+                       "parallelism": f"channel-shard x{world}",
                        "dist_backend": backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

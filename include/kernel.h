@@ -56,6 +56,7 @@ inline pv_handle* compat_handle(int N, int hop) {
     auto it = cache.find({N, hop, nf});
     if (it != cache.end()) return it->second;
     pv_config cfg{};
+    cfg.abi_version = PV_ABI_VERSION;
     cfg.n_samps = N;
     cfg.hop_div = (hop > 0 && N % hop == 0) ? N / hop : 2;
     cfg.effect = PV_TIME_SHIFT;
@@ -74,6 +75,7 @@ inline pv_handle* compat_handle(int N, int hop) {
 }
 inline int spec_stride(pv_handle* h) {
     pv_info info{};
+    info.abi_version = PV_ABI_VERSION;
     pv_get_info(h, &info);
     return info.spec_stride;
 }

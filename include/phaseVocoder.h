@@ -199,6 +199,7 @@ class PhaseVocoder {
     void init(int samples, Effect e, float scaleFactor, int hop, pv_mode mode, int window,
               int max_channels, int max_frames, int device) {
         pv_config cfg{};
+        cfg.abi_version = PV_ABI_VERSION;
         cfg.n_samps = samples;
         cfg.hop_div = hop;
         cfg.effect = (int)e;
@@ -211,6 +212,7 @@ class PhaseVocoder {
         cfg.nan_faithful = CudaPhase::detail::nan_faithful_flag();
         checkCUDAErrori(pv_create(&cfg, &handle), "PhaseVocoder constructor", __LINE__);
         pv_info info{};
+        info.abi_version = PV_ABI_VERSION;
         pv_get_info(handle, &info);
         nSamps = N = info.n_samps;
         hopSize = info.hop;

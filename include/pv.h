@@ -42,9 +42,12 @@
 extern "C" {
 #endif
 
-#define PV_ABI_VERSION 3  /* 2: pv_config.window / nan_faithful, pv_set_window;
-                             3: pv_info.single_launch / single_launch_frames / lane_constants,
-                                pv_check_device */
+#define PV_ABI_VERSION 4  /* 2: pv_config.window / nan_faithful, pv_set_window;
+                             3: pv_info.single_launch / single_launch_frames / lane_constants;
+                             4: leading abi_version in pv_config / pv_info (checked: a caller
+                                built against another header gets PV_ERR_ARG, not a
+                                misread struct), pv_config.spec_layout, the chained path
+                                and pv_check_device removed */
 
 typedef struct pv_handle pv_handle;
 
@@ -71,6 +74,18 @@ typedef enum pv_mode {
     PV_MODE_STANDARD = 1    /* textbook phase vocoder (Hann, unwrap, true frequency)     */
 } pv_mode;
 
+/* STANDARD spectrum row layout (pv_config.spec_layout) */
+typedef enum pv_spec_layout {
+    PV_SPEC_NATURAL = 0, /* {mag, phase} of bins k = 0 .. N/2 (spec_bins = N/2+1), rows padded
+                            to spec_stride = N/2 + 8                                          */
+    PV_SPEC_PACKED = 1   /* rows of exactly N/2 float2 (spec_stride = spec_bins = N/2): bins
+                            1 .. N/2-1 as {mag, phase}; bin 0 and bin N/2, both real, share
+                            slot 0 as {s0, sN/2} with s = +mag for phase 0, -mag for phase pi
+                            (the sign bit carries the phase; pv_unpack_bins below).  Every
+                            row store is whole 64-byte segments (no 8-byte partial write for
+                            bin N/2).  STANDARD handles only; the real-time mode rejects it */
+} pv_spec_layout;
+
 typedef enum pv_window {
     PV_WINDOW_DEFAULT = 0,     /* the mode's window: REF_COMPAT the symmetric Hamming of the
                                   4-argument constructor, STANDARD the periodic Hann        */
@@ -81,6 +96,7 @@ typedef enum pv_window {
 } pv_window;
 
 typedef struct pv_config {
+    int abi_version;  /* = PV_ABI_VERSION (pv_create rejects any other value)          */
     int n_samps;      /* N, window length: power of 2 in [256, 2048] (both modes)       */
     int hop_div;      /* hop = N / hop_div (phaseVocoder.h:79 4th argument is a divisor)  */
     int effect;       /* pv_effect                                                      */
@@ -93,11 +109,14 @@ typedef struct pv_config {
     int nan_faithful; /* REF_COMPAT: a bin with Re = Im = 0 gets phase atanf(0/0) = NaN as
                          in the reference (kernel.cu:101-109), which poisons that frame's
                          resynthesis; 0 (default) gives phase 0 (SURVEY.md §8c deviation 4) */
+    int spec_layout;  /* pv_spec_layout (STANDARD only; REF_COMPAT accepts 0)              */
 } pv_config;
 
 typedef struct pv_info {
+    int abi_version;    /* the caller sets PV_ABI_VERSION (pv_get_info checks it)           */
     int n_samps, hop, out_hop;
-    int spec_bins;      /* bins written per frame: N/2+1 (STANDARD) or 2N (REF_COMPAT)  */
+    int spec_bins;      /* slots written per frame: N/2+1 (STANDARD natural), N/2 (STANDARD
+                           packed) or 2N (REF_COMPAT)                                     */
     int spec_stride;    /* pv_float2 elements between consecutive frames of a channel   */
     int frames_per_run; /* frames per wave run; chosen from           */
                         /* max_channels x max_frames, or the environment variable       */
@@ -111,7 +130,25 @@ typedef struct pv_info {
                                  in registers (e_k and (p j_k) mod q repeat every 64 bins:
                                  64 a multiple of N / hop and q of 64 hop / N, e.g. config
                                  3 and 4); PV_SYN_LANEK=0 read by pv_create turns it off  */
+    int spec_layout;          /* pv_spec_layout of the handle's spectrum rows               */
 } pv_info;
+
+/* A PV_SPEC_PACKED row's slot 0 -> {mag, phase} of bin 0 and bin N/2.  Exact: the packed
+ * phases are +0 or the float nearest pi (0x1.921fb6p+1f) and the magnitude is the sign-free
+ * slot value. */
+static inline void pv_unpack_bins(pv_float2 slot0, pv_float2* bin0, pv_float2* bin_half) {
+    const float pi = 0x1.921fb6p+1f;
+    union { float f; unsigned u; } a, b;
+    a.f = slot0.x;
+    b.f = slot0.y;
+    const unsigned sa = a.u >> 31, sb = b.u >> 31;
+    a.u &= 0x7fffffffu;
+    b.u &= 0x7fffffffu;
+    bin0->x = a.f;
+    bin0->y = sa ? pi : 0.0f;
+    bin_half->x = b.f;
+    bin_half->y = sb ? pi : 0.0f;
+}
 
 int pv_abi_version(void);
 const char* pv_status_string(pv_status s);

@@ -22,7 +22,8 @@ namespace pv {
 // D > 0: hop = 128 D samples, so frame u+1's register q is frame u's register q + D and a
 // frame costs only its D new sample pairs per lane (the other E - D are shifted in
 // registers): 1/E of the frame's bytes leave L2 instead of all of them.
-template <int L, bool EKL, int D = 0>
+// PACKED: the pv.h PV_SPEC_PACKED row layout (bin L folded into slot 0).
+template <int L, bool EKL, int D, bool PACKED>
 __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? PV_ANA_WAVES1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
@@ -37,11 +38,7 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     float* ekl = winl + N;                            // B
 
     const int tid = threadIdx.x, lane = tid & 63;
-    #ifdef PV_NO_RFL_ANA
-    const int w = tid >> 6;
-#else
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
-#endif
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
     for (int i = tid; i < TWN; i += 256) twl[i] = p.tw[i];
@@ -60,8 +57,8 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
     // it is known, S after the loop
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * 2 * p.bins_pad : nullptr;
     float phprev[E + 1], sacc[E + 1];
-    ana_run<L, EKL, D, (bool)PV_NT_SPEC>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c,
-                                        t0, nfr, e_lane, rec, phprev, sacc);
+    ana_run<L, EKL, D, PACKED>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c, t0, nfr,
+                               e_lane, rec, phprev, sacc);
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT
@@ -153,19 +150,25 @@ static size_t ana_lds_compat() {
         default: return hipErrorInvalidValue;         \
     }
 
-hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
-    dim3 grid((p.nruns + 3) / 4, channels);
+template <bool PK>
+static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hipStream_t s) {
     PV_DISPATCH_L(L, {
+        // shifted-register input when hop = 128 D (D < E)
         const int d = (p.aligned && p.hop % 128 == 0) ? p.hop / 128 : 0;
-        if (PV_ANA_SHIFT && p.ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
+        if (p.ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
             constexpr int E_ = LL / 64;  // D < E (instantiated for every L, run for the checked ones)
-            if (d == 1) hipLaunchKernelGGL((k_std_analysis<LL, false, (1 < E_) ? 1 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-            else if (d == 2) hipLaunchKernelGGL((k_std_analysis<LL, false, (2 < E_) ? 2 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-            else hipLaunchKernelGGL((k_std_analysis<LL, false, (4 < E_) ? 4 : 0>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-        } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-        else hipLaunchKernelGGL((k_std_analysis<LL, true>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
+            if (d == 1) hipLaunchKernelGGL((k_std_analysis<LL, false, (1 < E_) ? 1 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+            else if (d == 2) hipLaunchKernelGGL((k_std_analysis<LL, false, (2 < E_) ? 2 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+            else hipLaunchKernelGGL((k_std_analysis<LL, false, (4 < E_) ? 4 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+        } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false, 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+        else hipLaunchKernelGGL((k_std_analysis<LL, true, 0, PK>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });
     return hipGetLastError();
+}
+
+hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
+    const dim3 grid((p.nruns + 3) / 4, channels);
+    return p.packed ? launch_std_analysis_t<true>(L, grid, p, s) : launch_std_analysis_t<false>(L, grid, p, s);
 }
 
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {

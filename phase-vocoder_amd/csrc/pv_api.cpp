@@ -103,6 +103,7 @@ struct pv_handle {
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
+    int packed = 0;  // PV_SPEC_PACKED rows (STANDARD)
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
     unsigned long long p_mod = 0, q = 1;
     int q_pow2 = 1;
@@ -116,7 +117,6 @@ struct pv_handle {
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
     int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
-    unsigned long long* d_clk = nullptr;  // PV_CLOCK_PROBE builds only
     Profile prof;
 };
 
@@ -217,7 +217,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.runsum = want_runsum ? h->d_runsum : nullptr;
     p.bins_pad = h->bins_pad;
     p.nan_faithful = h->nan_faithful;
-    p.clk = h->d_clk;
+    p.packed = h->packed;
     if (h->mode == PV_MODE_STANDARD)
         PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
     else
@@ -254,6 +254,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
         sc.nruns = nruns;
         sc.L = h->L_syn;
         sc.bins_pad = h->bins_pad;
+        sc.packed = h->packed;
         sc.ek = h->d_ek;
         sc.runsum = h->d_runsum;
         sc.carry = h->d_carry;
@@ -291,6 +292,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.tails = h->d_tails;
     p.tail_len = h->tail_len;
     p.k_lane = h->k_lane;
+    p.packed = h->packed;
     const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
     PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, smode, C, p, s));
     const int nwg = (nruns + 3) / 4;
@@ -352,6 +354,7 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     p.tails = h->d_tails;
     p.tail_len = h->tail_len;
     p.seam_flags = h->d_seam_flags;
+    p.packed = h->packed;
     PV_LAUNCH(h, KF, s, pv::launch_fused(h->L_syn, h->pitch ? 2 : 0, C, p, s));
     return PV_OK;
 }
@@ -390,6 +393,8 @@ long long pv_output_length(const pv_handle* h, int frames) {
 
 pv_status pv_get_info(const pv_handle* h, pv_info* info) {
     if (!h || !info) return fail(PV_ERR_ARG, "null argument");
+    if (info->abi_version != PV_ABI_VERSION)
+        return fail(PV_ERR_ARG, "pv_info.abi_version != PV_ABI_VERSION (caller built against another pv.h)");
     info->n_samps = h->N;
     info->hop = h->hop;
     info->out_hop = h->hs;
@@ -402,6 +407,7 @@ pv_status pv_get_info(const pv_handle* h, pv_info* info) {
     info->single_launch = h->F_fused > 0 ? 1 : 0;
     info->single_launch_frames = h->F_fused;
     info->lane_constants = h->k_lane;
+    info->spec_layout = h->packed ? PV_SPEC_PACKED : PV_SPEC_NATURAL;
     return PV_OK;
 }
 
@@ -410,7 +416,7 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_clk};
+                    h->d_carry, h->d_tails, h->d_seam_flags};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
@@ -422,6 +428,8 @@ void pv_destroy(pv_handle* h) {
 pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if (!cfg || !out) return fail(PV_ERR_ARG, "null argument");
     *out = nullptr;
+    if (cfg->abi_version != PV_ABI_VERSION)
+        return fail(PV_ERR_ARG, "pv_config.abi_version != PV_ABI_VERSION (caller built against another pv.h)");
     const int N = cfg->n_samps;
     if (!is_pow2(N)) return fail(PV_ERR_UNSUPPORTED, "n_samps must be a power of two");
     if (cfg->mode != PV_MODE_STANDARD && cfg->mode != PV_MODE_REF_COMPAT)
@@ -439,6 +447,10 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         return fail(PV_ERR_ARG, "unknown window");
     if (cfg->mode == PV_MODE_STANDARD && cfg->window != PV_WINDOW_DEFAULT)
         return fail(PV_ERR_UNSUPPORTED, "STANDARD mode: the periodic Hann window only (window = 0)");
+    if (cfg->spec_layout != PV_SPEC_NATURAL && cfg->spec_layout != PV_SPEC_PACKED)
+        return fail(PV_ERR_ARG, "unknown spec_layout");
+    if (cfg->spec_layout == PV_SPEC_PACKED && cfg->mode != PV_MODE_STANDARD)
+        return fail(PV_ERR_UNSUPPORTED, "PV_SPEC_PACKED: STANDARD handles only");
 
     pv_handle* h = new pv_handle();
     h->cfg = *cfg;
@@ -470,7 +482,9 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     h->L_ana = (h->mode == PV_MODE_STANDARD) ? N / 2 : N;
     h->bins = N / 2 + 1;
     h->bins_pad = (h->bins + 7) & ~7;
-    h->spec_bins = (h->mode == PV_MODE_STANDARD) ? h->bins : 2 * N;
+    h->packed = (cfg->spec_layout == PV_SPEC_PACKED) ? 1 : 0;
+    // packed rows are exactly N/2 float2: bin N/2 rides in slot 0
+    h->spec_bins = (h->mode == PV_MODE_STANDARD) ? (h->packed ? N / 2 : h->bins) : 2 * N;
     h->spec_stride = (h->spec_bins + 7) & ~7;
     if (h->L_ana > 2048 || h->L_syn > 2048 || h->L_syn < 128) {
         delete h;
@@ -602,16 +616,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
 
     // ---- single-launch path (q = 1): no halo frame, so runs can be as short as the overlap
     // tail allows (F hs >= N - hs) to give a single stream enough waves; PV_FUSED=0 disables
-    // it (A/B), PV_FUSED_FRAMES overrides its run length
-#ifdef PV_TIMING_PROBES
-    // PV_FUSED_FORCE=1 (timing probe builds only, output WRONG for q > 1): runs the q = 1
-    // kernel on any STANDARD geometry to bound what a single-launch path could reach there
-    const char* ff = std::getenv("PV_FUSED_FORCE");
-    const bool force_fused = ff && ff[0] == '1';
-#else
-    const bool force_fused = false;
-#endif
-    if (h->mode == PV_MODE_STANDARD && (h->q == 1 || force_fused) && pv::fused_supported(h->L_syn, h->hs)) {
+    // it (tests compare both paths), PV_FUSED_FRAMES overrides its run length
+    if (h->mode == PV_MODE_STANDARD && h->q == 1 && pv::fused_supported(h->L_syn, h->hs)) {
         const int fmin = std::max(2, (h->tail_len + h->hs - 1) / h->hs);
         int Ff = (int)std::min<long long>(h->F, std::max<long long>(fmin, work / 4096));
         if (const char* ev = std::getenv("PV_FUSED_FRAMES")) {
@@ -636,10 +642,6 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         PV_HIP(hipMalloc((void**)&h->d_seam_flags, sizeof(int) * wg_total));
         PV_HIP(hipMemset(h->d_seam_flags, 0, sizeof(int) * wg_total));
     }
-#ifdef PV_CLOCK_PROBE
-    PV_HIP(hipMalloc((void**)&h->d_clk, sizeof(unsigned long long) * 2 * runs_total));
-    PV_HIP(hipMemset(h->d_clk, 0, sizeof(unsigned long long) * 2 * runs_total));
-#endif
 
     // LDS budget check for the synthesis kernel (largest)
     size_t lds = pv::synthesis_lds_bytes(h->L_syn, h->hs);
@@ -774,16 +776,6 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
     PV_HIP(hipStreamSynchronize(s));
     return PV_OK;
 }
-
-#ifdef PV_CLOCK_PROBE
-// diagnostic builds only (not declared in pv.h): the per-wave {memtime, realtime} deltas
-// of the last analysis launch, 2 * channels * runs values
-pv_status pv_debug_clock(pv_handle* h, unsigned long long* host, size_t n) {
-    if (!h || !host || !h->d_clk) return fail(PV_ERR_ARG, "no clock buffer");
-    PV_HIP(hipMemcpy(host, h->d_clk, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
-    return PV_OK;
-}
-#endif
 
 pv_status pv_set_window(pv_handle* h, const float* win, void* stream) {
     if (!h || !win) return fail(PV_ERR_ARG, "null argument");
@@ -926,6 +918,8 @@ pv_status pv_rt_create(const pv_config* cfg, int channels, pv_rt** out) {
     *out = nullptr;
     if (cfg->mode != PV_MODE_STANDARD)
         return fail(PV_ERR_UNSUPPORTED, "real-time mode runs the STANDARD pipeline only");
+    if (cfg->spec_layout != PV_SPEC_NATURAL)
+        return fail(PV_ERR_UNSUPPORTED, "real-time mode: natural spectrum rows only");
     if (channels <= 0) return fail(PV_ERR_ARG, "channels must be > 0");
     pv_config c = *cfg;
     c.max_channels = channels;

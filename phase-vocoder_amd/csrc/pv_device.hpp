@@ -76,31 +76,6 @@ __device__ __forceinline__ f2v cmul_v(f2v b, f2v w) {
     return t;
 }
 
-// Packed-operand helpers (VOP3P modifiers do the swizzles and sign flips, so no register
-// copies are needed to assemble operand pairs).  Each is one instruction and rounds once
-// per lane exactly like the scalar op it replaces.
-__device__ __forceinline__ f2v pk_add(f2v a, f2v b) {
-    f2v r;
-    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ f2v pk_sub(f2v a, f2v b) {  // (a.x - b.x, a.y - b.y)
-    f2v r;
-    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ f2v pk_half(f2v a) {  // (0.5 a.x, 0.5 a.y)
-    f2v r;
-    asm("v_pk_mul_f32 %0, %1, 0.5 op_sel_hi:[1,0]" : "=v"(r) : "v"(a));
-    return r;
-}
-// (lo of a, hi of b)
-__device__ __forceinline__ f2v pk_lo_hi(f2v a, f2v b) {
-    f2v r;
-    asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
 // top + (bot.y, -bot.x) [NEG = false] or top - (bot.y, -bot.x) = top + (-bot.y, bot.x)
 // [NEG = true]: the -i (or +i) butterfly of stage Ns = 2 with the swap and sign in the
 // VOP3P modifiers; each lane op is the single rounding of the scalar form.
@@ -151,10 +126,8 @@ __device__ __forceinline__ void gload_pairs(f2v (&xr)[E], const float* src) {
                          : "=v"(xr[q]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
-#ifndef PV_NT_INPUT
-#define PV_NT_INPUT 0  // non-temporal input loads: measured +0.1 % (noise), off
-#endif
-// the last D pairs of gload_pairs<E>: registers q = E-D .. E-1
+// the last D pairs of gload_pairs<E>: registers q = E-D .. E-1 (plain loads: non-temporal
+// ones measured +0.1 %, noise)
 template <int D, int E>
 __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
 #pragma unroll
@@ -162,28 +135,37 @@ __device__ __forceinline__ void gload_tail(f2v (&xr)[D], const float* src) {
         constexpr int Q0 = E - D;
         const int q = Q0 + j;
         const float* pq = src + 1024 * (q >> 3);
-        if constexpr ((bool)PV_NT_INPUT)  // each sample pair is read once here
-            asm volatile("global_load_dwordx2 %0, %1, off offset:%2 nt"
-                         : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
-        else
-            asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
-                         : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
+        asm volatile("global_load_dwordx2 %0, %1, off offset:%2"
+                     : "=v"(xr[j]) : "v"(pq), "n"(512 * (q & 7)) : "memory");
     }
 }
-#ifndef PV_NT_ROWS
-#define PV_NT_ROWS 1  // measured +0.4 % (config 3)
-#endif
-// one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and bin L (the
-// same address on every lane) from rowL
-template <int E, bool NT = (bool)PV_NT_ROWS>
-__device__ __forceinline__ void gload_row(f2v (&v)[E + 1], const float2* rowlane, const float2* rowL) {
+// one spectrum row: bins lane + 64 q (q < E) from rowlane = row + lane, and (bin_l) bin L
+// (the same address on every lane) from rowL.  Rows are read exactly once: NT streams them
+// past the caches (measured +0.4 % on config 3).
+template <int E, bool NT = true>
+__device__ __forceinline__ void gload_row(f2v (&v)[E + 1], const float2* rowlane, const float2* rowL,
+                                          bool bin_l = true) {
     f2v (&head)[E] = *reinterpret_cast<f2v(*)[E]>(&v[0]);
-    // rows are read exactly once: NT (PV_NT_ROWS) streams them past the caches
     gload_pairs<E, NT>(head, reinterpret_cast<const float*>(rowlane));
-    if constexpr (NT)
-        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v[E]) : "v"(rowL) : "memory");
-    else
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");
+    if (bin_l) {
+        if constexpr (NT)
+            asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v[E]) : "v"(rowL) : "memory");
+        else
+            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v[E]) : "v"(rowL) : "memory");
+    }
+}
+
+// PV_SPEC_PACKED slot value of a real bin (bins 0 and L: Im = +0, so the contract's phase is
+// +0 or pi): the magnitude with the sign bit set for phase pi
+__device__ __forceinline__ float pack_real_bin(float mag, float ph) { return ph > 0.0f ? -mag : mag; }
+// slot 0 {s0, sL} -> {mag, phase} of bins 0 and L: the magnitude is the sign-free value, the
+// phase +0 or pi by the sign bit (exactly the analysis's phases)
+__device__ __forceinline__ void unpack_real_bins(float2 s, float2& b0, float2& bL) {
+    constexpr float pi = 0x1.921fb6p+1f;  // kPi (declared below)
+    const float p0 = (__float_as_uint(s.x) >> 31) ? pi : 0.0f;
+    const float pL = (__float_as_uint(s.y) >> 31) ? pi : 0.0f;
+    b0 = make_float2(__builtin_fabsf(s.x), p0);
+    bL = make_float2(__builtin_fabsf(s.y), pL);
 }
 template <int K, int E>
 __device__ __forceinline__ void vm_wait(f2v (&xr)[E]) {
@@ -199,9 +181,6 @@ __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
     return t;
 }
 
-#ifndef PV_ATAN_IEEE_DIV
-#define PV_ATAN_IEEE_DIV 0  // must match the oracle's contract (it uses the division-free form)
-#endif
 // atan2 of the contract (oracle pvr_atan2f); atan(a) = a*P(a^2), |err| <= 2.7e-7 rad.
 // Zero bins: +-0 (the sign of y); y = -0 gives -phase like C's atan2.
 __device__ __forceinline__ float atan2_pv(float y, float x) {
@@ -214,9 +193,6 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     float mx, mn;
     asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(mx) : "v"(x), "v"(y), "s"(0x1p-126f));
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
-#if PV_ATAN_IEEE_DIV
-    float a = mn / mx;  // IEEE division (-fhip-fp32-correctly-rounded-divide-sqrt)
-#else
     // a = mn / mx by the contract's division-free reciprocal (oracle pvr_atan2f): integer
     // seed + three fmaf Newton steps + one product (8 VALU, no v_rcp / div_scale chain)
     float r = __uint_as_float(0x7EF311C3u - __float_as_uint(mx));
@@ -227,7 +203,6 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     e = __builtin_fmaf(-mx, r, 1.0f);
     r = __builtin_fmaf(r, e, r);
     float a = mn * r;
-#endif
     float s = a * a;
     float p = -0x1.8ba68ap-10f;
     p = __builtin_fmaf(p, s, 0x1.398008p-7f);
@@ -245,52 +220,14 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     return __builtin_copysignf(rr, y);  // rr >= 0 here: the sign of y (v_bfi_b32)
 }
 
-// sin/cos for the bounded phases of the synthesis (|x| < 2^10): Cody-Waite reduction by
-// pi/2 in three parts + minimax polynomials on [-pi/4, pi/4] (cephes sinf/cosf
-// coefficients); |err| <= ~1.2e-7.  Replaces ocml sincosf, whose huge-argument path costs
-// registers the synthesis kernel needs for occupancy.  Not part of the bit-exact
-// contract (synthesis parity is tolerance based).
-__device__ __forceinline__ void sincos_pv(float x, float* sn, float* cs) {
-    const float j = __builtin_rintf(x * 0x1.45f306p-1f);  // x * 2/pi
-    float r = __builtin_fmaf(-j, 1.5703125f, x);
-    r = __builtin_fmaf(-j, 4.837512969970703125e-4f, r);
-    r = __builtin_fmaf(-j, 7.54978995489188216e-8f, r);
-    const float r2 = r * r;
-    float ps = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
-    ps = __builtin_fmaf(r2, ps, -1.6666654611e-1f);
-    const float s = __builtin_fmaf(r * r2, ps, r);
-    float pc = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
-    pc = __builtin_fmaf(r2, pc, 4.166664568298827e-2f);
-    const float c = __builtin_fmaf(r2 * r2, pc, __builtin_fmaf(-0.5f, r2, 1.0f));
-    const int q = ((int)j) & 3;
-    const float sv = (q & 1) ? c : s;
-    const float cv = (q & 1) ? s : c;
-    *sn = (q & 2) ? -sv : sv;
-    *cs = ((q + 1) & 2) ? -cv : cv;
-}
-
-#ifndef PV_HW_REDUCE
-#define PV_HW_REDUCE 1  // measured: synthesis -2.5 %
-#endif
-// sin/cos of 2 pi rev.  Default: the hardware v_sin_f32 / v_cos_f32 (inputs in
-// revolutions, quarter-rate transcendental) after an exact reduction to [-1/2, 1/2]
-// (rev - rint(rev) is exact for |rev| < 2^23); PV_SOFT_SINCOS selects the polynomial
-// sincos_pv.  Synthesis parity is tolerance based, so either is in
-// contract; the GPU tests bound the end-to-end error.
+// sin/cos of 2 pi rev: the hardware v_sin_f32 / v_cos_f32 (inputs in revolutions,
+// quarter-rate transcendental; they reduce their input themselves over [-256, 256]
+// revolutions, and every caller passes |rev| < 4: output phases are carried reduced;
+// measured: synthesis -2.5 % against an explicit rev - rint(rev)).  Synthesis parity is
+// tolerance based; the GPU tests bound the end-to-end error.
 __device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
-#if PV_HW_REDUCE
-    // v_sin/v_cos reduce their input themselves over [-256, 256] revolutions; every
-    // caller passes |rev| < 4 (output phases are carried reduced)
-    const float r = rev;
-#else
-    const float r = rev - __builtin_rintf(rev);
-#endif
-#ifdef PV_SOFT_SINCOS
-    sincos_pv(r * kTwoPi, sn, cs);
-#else
-    *sn = __builtin_amdgcn_sinf(r);
-    *cs = __builtin_amdgcn_cosf(r);
-#endif
+    *sn = __builtin_amdgcn_sinf(rev);
+    *cs = __builtin_amdgcn_cosf(rev);
 }
 
 // unwrap decision of the contract (oracle pvr_unwrap_count)

@@ -14,9 +14,6 @@
 #include "pv_device.hpp"
 #include "pv_kernels.h"
 
-#ifndef PV_FFT_SMALL_LDS
-#define PV_FFT_SMALL_LDS 0  // 1: the per-stage LDS kernel for N <= 64 (previous form)
-#endif
 
 namespace pv {
 
@@ -160,10 +157,6 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
         case 2048: PV_FFT_L(2048); break;
         default: {
             if (n < 2 || n > 64 || (n & (n - 1))) return hipErrorInvalidValue;
-#if PV_FFT_SMALL_LDS
-            if (inverse) hipLaunchKernelGGL((k_fft_small<true>), grid, block, 0, s, in, out, tw, n, batch);
-            else hipLaunchKernelGGL((k_fft_small<false>), grid, block, 0, s, in, out, tw, n, batch);
-#else
             // in-place use reads each lane's transform completely before writing it: safe;
             // 16-byte vector access needs 16-byte aligned buffers (n >= 4)
             if (n >= 4 && ((((uintptr_t)in) | ((uintptr_t)out)) & 15)) {
@@ -179,7 +172,6 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
         break;
             switch (n) { PV_FFT_R(2) PV_FFT_R(4) PV_FFT_R(8) PV_FFT_R(16) PV_FFT_R(32) PV_FFT_R(64) }
 #undef PV_FFT_R
-#endif
         }
     }
 #undef PV_FFT_L

@@ -5,16 +5,6 @@
 #pragma once
 #include "pv_device.hpp"
 
-#ifndef PV_PK_SPLIT
-#define PV_PK_SPLIT 0  // packed-instruction real split (analysis): measured slower (latency)
-#endif
-#ifndef PV_SPLIT_BP
-#define PV_SPLIT_BP 1  // analysis real split from the last pass's registers via ds_bpermute
-                       // (split_chunk_bp) instead of a final image in LDS (split_chunk)
-#endif
-#ifndef PV_PK_PRESTEP
-#define PV_PK_PRESTEP 1  // packed-instruction inverse real-FFT pre-step (synthesis)
-#endif
 
 namespace pv {
 
@@ -64,27 +54,7 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
             tw[c] = lds_ld(&twsl[L]);
         }
     }
-#if PV_PK_SPLIT
-    // packed form, same roundings: S = A + B, D = A - B; H = S/2 = (er, or); G = D/2 =
-    // (-oi, ei); P = (oi tw.y, oi tw.x) = (-G.x tw.y, -G.x tw.x) (sign flips are exact);
-    // T = (fma(or, tw.x, -P.x), fma(or, tw.y, P.y)); X = (er, ei) + T
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        const f2v a = f2v{A[c].x, A[c].y}, b = f2v{Bz[c].x, Bz[c].y}, w = f2v{tw[c].x, tw[c].y};
-        const f2v H = pk_half(pk_add(a, b));
-        const f2v G = pk_half(pk_sub(a, b));
-        f2v P, T;
-        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[1,0]"
-            : "=v"(P) : "v"(G), "v"(w));
-        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] neg_lo:[0,0,1]"
-            : "=v"(T) : "v"(H), "v"(w), "v"(P));
-        const f2v Xv = pk_add(pk_lo_hi(H, G), T);
-        float Xi = Xv.y;
-        if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
-        X[c] = make_float2(Xv.x, Xi);
-    }
-#else
+    // (scalar form: a packed-instruction split measured slower, latency-bound chains)
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int i = i0 + c;
@@ -98,7 +68,6 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
         X[c] = make_float2(Xr, Xi);
     }
-#endif
 }
 
 // register index holding slot c after the last FFT pass (inverse of last_slot)
@@ -109,14 +78,21 @@ constexpr int slot_reg(int c) {
     return -1;
 }
 
+// Order in which a frame's bins are split: 0, 1, .., E (bin L last), or with PACKED
+// 0, E, 1, .., E-1 (bins 0 and L in the first chunk: the packed row layout stores them in
+// one slot).
+template <int E, bool PACKED>
+constexpr int bin_at(int pos) { return !PACKED ? pos : pos == 0 ? 0 : pos == 1 ? E : pos - 1; }
+
 // split_chunk from the last FFT pass's registers instead of the natural-order image in LDS
 // (no final tile store, no tile reads): lane l holds Z[l + 64 c] in register slot_reg(c), so
 // A = Z[k], k = l + 64 i, is the lane's own register and B = Z[(L - k) mod L] =
 // Z[(64 - l) + 64 (E - 1 - i)] is register slot E-1-i of lane 64 - l — a lane reversal by
 // ds_bpermute (crossbar only).  Lane 0's partners are its own registers (Z[(L - 64 i) mod L]
 // = slot (E - i) mod E): it selects them before the permute and reads from itself.  Same
-// operands, same operations as split_chunk: bit-identical bins.
-template <int L, int CH, bool TWICE, int I0>
+// operands, same operations as split_chunk: bit-identical bins.  Chunk positions P0 ..
+// P0 + CH - 1 are bins bin_at<E, PACKED>(position) (positions past E are dummies).
+template <int L, int CH, bool TWICE, int P0, bool PACKED = false>
 __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], const float2* twsl, int lane,
                                                float2 (&X)[CH]) {
     constexpr int E = Geo<L>::E;
@@ -126,7 +102,7 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
     float2 A[CH], Bz[CH], tw[CH];
     static_for<0, CH>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        constexpr int i = I0 + c;
+        constexpr int i = (P0 + c <= E) ? bin_at<E, PACKED>(P0 + c) : E;
         if constexpr (i < E) {
             A[c] = v[slot_reg<L>(i)];
             const float2 o = v[slot_reg<L>(E - 1 - i)];
@@ -145,9 +121,9 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
             tw[c] = lds_ld(&twsl[L]);
         }
     });
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int i = I0 + c;
+    static_for<0, CH>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int i = (P0 + c <= E) ? bin_at<E, PACKED>(P0 + c) : E;
         constexpr float h = TWICE ? 1.0f : 0.5f;
         const float er = h * (A[c].x + Bz[c].x);
         const float ei = h * (A[c].y - Bz[c].y);
@@ -157,7 +133,7 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
         float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
         X[c] = make_float2(Xr, Xi);
-    }
+    });
 }
 
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
@@ -378,7 +354,8 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         float2 tw;  // e^{-2 pi i k/N}, k = lane + 64 q
         if constexpr (TwS::ON) tw = twr.v[q];
         else tw = lds_ld(&twsl[lane + 64 * q]);
-#if PV_PK_PRESTEP
+        // packed pre-step, same roundings as the scalar form fer - Foi, fei + For with
+        // For = fma(dr, tw.x, di tw.y), Foi = fma(di, tw.x, -(dr tw.y)).
         // V = (dr, di) = (A.x - B.x, A.y + B.y), W = (fer, fei) = (A.x + B.x, A.y - B.y):
         // one v_pk_add each, the sign flips by neg_lo / neg_hi;
         // R = (di tw.y, -(dr tw.y)); Q = (For, Foi) = V tw.x + R; z = (fer - Foi, fei + For)
@@ -390,13 +367,6 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(Q) : "v"(V), "v"(w), "v"(R));
         asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(Z) : "v"(W), "v"(Q));
         z[q] = make_float2(Z.x, Z.y);
-#else
-        const float fer = A.x + Bc.x, fei = A.y - Bc.y;  // A + conj(B)
-        const float dr = A.x - Bc.x, di = A.y + Bc.y;    // A - conj(B)
-        const float For = __builtin_fmaf(dr, tw.x, di * tw.y);   // (A - conj B) conj(tw)
-        const float Foi = __builtin_fmaf(di, tw.x, -(dr * tw.y));
-        z[q] = make_float2(fer - Foi, fei + For);
-#endif
     }
     wave_lds_sync();
     fft_run<L, true, STORE_LAST>(z, tile, twl, tw0, lane);

@@ -21,11 +21,6 @@
 // second of the two workgroups to finish (no k_seam launch).
 #include "pv_syn_run.hpp"
 
-#ifndef PV_FUSED_SPLIT_BP
-#define PV_FUSED_SPLIT_BP 0  // the register split (split_chunk_bp) costs this kernel 2 VGPRs over
-                             // 128 at L = 512 (3 waves/SIMD, or spills at 4): config 2 +2-3 %
-#endif
-
 namespace pv {
 
 // Inter-workgroup hand-offs: st_sc1 / ld_sc1 / arrive / close_seams_inline (pv_syn_run.hpp),
@@ -142,16 +137,18 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
                 }
             }
             if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
-            // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv
-            fft_run<L, false, !PV_FUSED_SPLIT_BP>(z, tile, twl, tw0, lane);
+            // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv.  The
+            // split reads the final image in LDS (the register split, split_chunk_bp, costs
+            // this kernel 2 VGPRs over 128 at L = 512: 3 waves/SIMD, or spills at 4; config 2
+            // +2-3 %)
+            fft_run<L, false, true>(z, tile, twl, tw0, lane);
             float2 sv[E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
             constexpr int CH = 3;
             static_for<0, (E + CH) / CH>([&](auto ic) {
                 constexpr int i0 = decltype(ic)::value * CH;
                 float2 X[CH];
-                if constexpr ((bool)PV_FUSED_SPLIT_BP) split_chunk_bp<L, CH, true, i0>(z, twsl, lane, X);
-                else split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
+                split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
 #pragma unroll
                 for (int c2 = 0; c2 < CH; ++c2) {
                     const int i = i0 + c2;
@@ -160,10 +157,19 @@ __global__ __launch_bounds__(256) void k_fused(FusedParams p) {
                     float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                     mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
                     sv[i] = make_float2(mag, ph);
-                    // bin L (i = E): the same value and address on every lane
-                    __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+                    // bin L (i = E): the same value and address on every lane (natural layout
+                    // only; packed rows carry it in slot 0); bins 0..63 go out below
+                    if (i > 0 && (i < E || !p.packed))
+                        __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
                 }
             });
+            {
+                // slot 0: PV_SPEC_PACKED lane 0 carries bins 0 and L (both real)
+                const bool pk0 = p.packed && lane == 0;
+                const f2v s0 = pk0 ? f2v{pack_real_bin(sv[0].x, sv[0].y), pack_real_bin(sv[E].x, sv[E].y)}
+                                   : f2v{sv[0].x, sv[0].y};
+                __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+            }
             wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers
             synth_frame<L, MODE, false, true, false, false, true>(sv, false, 0u, M, phprev, pmap, stb, tw0, tile,

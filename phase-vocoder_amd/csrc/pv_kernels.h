@@ -21,13 +21,14 @@ struct AnaParams {
     int* runsum;            // [C][nruns][2][bins_pad] {S, m0} or nullptr
     int bins_pad;
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
-    unsigned long long* clk;  // PV_CLOCK_PROBE diagnostic builds: per wave {memtime, realtime} deltas
+    int packed;             // STANDARD rows in the PV_SPEC_PACKED layout (bin L in slot 0)
 };
 
 struct ScanParams {
     const float2* spec;
     long long ld_spec;
     int spec_stride, frames, F, nruns, L, bins_pad;
+    int packed;                        // PV_SPEC_PACKED rows
     const float* ek;
     int* runsum;
     int* carry;
@@ -58,6 +59,7 @@ struct SynParams {
     float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
     int tail_len;
     int k_lane;                        // e_k, (p j_k) mod q depend on k mod 64 only (syn_run LANEK)
+    int packed;                        // PV_SPEC_PACKED rows (bins 0 and L in slot 0)
 };
 
 // single-launch STANDARD path for q = 1 (pv_fused.hip)
@@ -83,6 +85,7 @@ struct FusedParams {
     float* tails;                      // [C][nwg][tail_len], nwg = ceil(nruns/4)
     int tail_len;
     int* seam_flags;                   // [C][nwg] arrival counters, 0 between launches
+    int packed;                        // PV_SPEC_PACKED rows
 };
 
 struct SeamParams {

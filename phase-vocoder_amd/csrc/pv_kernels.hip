@@ -25,15 +25,22 @@ __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
     if (k > p.L) return;
     const int t0 = run * p.F;
     const int nfr = min(p.F, p.frames - t0);
-    const float2* s = p.spec + (long long)c * p.ld_spec + (long long)t0 * p.spec_stride + k;
+    // PV_SPEC_PACKED rows: bins 0 and L are the sign bits of slot 0 {s0, sL}
+    const bool real_bin = p.packed && (k == 0 || k == p.L);
+    const float2* s = p.spec + (long long)c * p.ld_spec + (long long)t0 * p.spec_stride + (real_bin ? 0 : k);
+    auto phase = [&](long long u) {
+        const float2 v = s[u * p.spec_stride];
+        if (!real_bin) return v.y;
+        return (__float_as_uint(k == 0 ? v.x : v.y) >> 31) ? kPi : 0.0f;
+    };
     const float e = p.ek[k];
-    float prev = (t0 > 0) ? s[-(long long)p.spec_stride].y : 0.0f;
-    float ph = s[0].y;
+    float prev = (t0 > 0) ? phase(-1) : 0.0f;
+    float ph = phase(0);
     const int m0 = unwrap_count(ph, prev, e);
     prev = ph;
     int acc = 0;
     for (int u = 1; u < nfr; ++u) {
-        ph = s[(long long)u * p.spec_stride].y;
+        ph = phase(u);
         acc += unwrap_count(ph, prev, e);
         prev = ph;
     }
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 
     }
     constexpr int NS = SynTraits<L, MODE, DT, QPOW2>::NS, D = SynTraits<L, MODE, DT, QPOW2>::D;
     float2 acc[NS];
-    syn_run<L, MODE, DT, QPOW2, (bool)PV_NT_ROWS, LANEK>(
+    syn_run<L, MODE, DT, QPOW2, LANEK>(
         p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, M, phprev, acc);
     if constexpr (ROLA) {
         // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
@@ -308,7 +315,7 @@ hipError_t launch_window_gain(const float* win, float* dwin, float* gain, int n,
 template <int L>
 static size_t syn_lds(int dt) {
     const int ring_floats = (dt > 0) ? 0 : 4 * 2 * L;               // ROLA: tails alias the tiles
-    const int gain_floats = (PV_SYN_GREG && dt > 0 && (L <= 512 || (L == 1024 && dt == 4 && PV_SYN_GREG1024))) ? 0 : 2 * L;  // GREG
+    const int gain_floats = (dt > 0 && (L <= 512 || (L == 1024 && dt == 4))) ? 0 : 2 * L;  // syn_gains_in_regs
     return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) +
            sizeof(float) * (ring_floats + gain_floats) + sizeof(float) * 4 * (L + 1 + 3);
 }
@@ -391,15 +398,17 @@ static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParam
     return hipGetLastError();
 }
 
+// the QPOW2 kernels carry the output phase in the revolution accumulator (RACC), exact for
+// power-of-two q <= 4096
 bool synthesis_lane_kernel(int L, int mode, int hs, bool q_pow2, unsigned long long q) {
-    const bool qp = q_pow2 && q <= (PV_REV_ACC ? 4096ull : (1ull << 24));
+    const bool qp = q_pow2 && q <= 4096ull;
     return mode != 1 && qp && syn_dt(L, hs) != 0;
 }
 
 // mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
-    const bool qp = p.q_pow2 && p.q <= (PV_REV_ACC ? 4096ull : (1ull << 24));
+    const bool qp = p.q_pow2 && p.q <= 4096ull;
     const int dt = (mode == 1 || qp) ? syn_dt(L, p.hs) : 0;
     if (mode == 0) return qp ? launch_synthesis_mode<0, true>(L, dt, grid, p, s)
                              : launch_synthesis_mode<0, false>(L, dt, grid, p, s);

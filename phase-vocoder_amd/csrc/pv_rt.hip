@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
                 z[q].y = xv.y * wv.y;
             }
         }
-        fft_run<L, false, !PV_SPLIT_BP>(z, tile, twl, tw0, lane);  // PV_SPLIT_BP: the split reads the registers
+        fft_run<L, false, false>(z, tile, twl, tw0, lane);  // the split reads the last pass's registers
         float2 sv[E + 1];
         float2* srow = (p.spec != nullptr)
                            ? p.spec + (long long)c * p.ld_spec + (long long)f * p.spec_stride
@@ -128,8 +128,7 @@ __global__ __launch_bounds__(256) void k_rt(RtParams p) {
         static_for<0, (E + CH) / CH>([&](auto ic) {
             constexpr int i0 = decltype(ic)::value * CH;
             float2 X[CH];
-            if constexpr ((bool)PV_SPLIT_BP) split_chunk_bp<L, CH, false, i0>(z, twsl, lane, X);
-            else split_chunk<L, CH, false>(tile, twsl, lane, i0, X);
+            split_chunk_bp<L, CH, false, i0>(z, twsl, lane, X);
 #pragma unroll
             for (int c2 = 0; c2 < CH; ++c2) {
                 const int i = i0 + c2;

@@ -6,38 +6,13 @@
 #include "pv_frame.hpp"
 #include "pv_kernels.h"
 
-#ifndef PV_SYN_GREG
-#define PV_SYN_GREG 1  // register-resident synthesis gains (ROLA, L <= 512); PV_SYN_1BUF
-                       // needs them in LDS (0) to fit 4 waves/SIMD
-#endif
-#ifndef PV_NT_OUT
-#define PV_NT_OUT 1  // non-temporal output stores in the synthesis (-0.5 %)
-#endif
-#ifndef PV_REV_ACC
-#define PV_REV_ACC 1  // measured: synthesis -2.5 % (with PV_HW_REDUCE -4.7 %)
-#endif
-#ifndef PV_SYN_1BUF
-#define PV_SYN_1BUF 0  // single spectrum-row buffer, next row issued mid-frame.  With
-                       // PV_SYN_GREG=0 PV_SYN_WAVES512=4: 118-120 VGPRs, 4 waves/SIMD instead of
-                       // 3; config 3 synthesis -5 % but the analysis +2 % (the denser
-                       // synthesis lowers the chip's clock for both), step +1.1 %
-                       // (profiles/r02_ab_layout_pf2.txt): off, the analysis is the roofline kernel
-#endif
-#ifndef PV_SYN_GREG1024
-#define PV_SYN_GREG1024 1  // ... and at L = 1024 with out hop 512 (config 4: 252 VGPRs, free below
-                           // the 2 waves/SIMD LDS sets; smaller out hops would need AGPRs)
-#endif
-#ifndef PV_SYN_TWREG
-#define PV_SYN_TWREG 1  // L = 1024 synthesis: split twiddles in registers (syn_run)
-#endif
-#ifndef PV_SYN_TWREG512
-#define PV_SYN_TWREG512 1  // ... and at L = 512 (config 3), within its 3 waves/SIMD budget
-#endif
-#ifndef PV_SYN_KREG
-#define PV_SYN_KREG 0  // measured: no gain over the LDS reads
-#endif
-
 namespace pv {
+
+// Register-resident synthesis gains (the register overlap-add kernels, L <= 512, and L = 1024
+// with out hop 512: config 4, 252 VGPRs, free below the 2 waves/SIMD its LDS sets; smaller
+// out hops would need AGPRs).
+template <int L, int DT>
+constexpr bool syn_gains_in_regs() { return DT > 0 && (L <= 512 || (L == 1024 && DT == 4)); }
 
 // sc1 (write-through) stores / loads of the inter-workgroup hand-offs (pv_fused.hip;
 // MI355X_MICROARCH.md "Valid forms")
@@ -149,20 +124,21 @@ struct SynTraits {
     static constexpr int E = Geo<L>::E;
     static constexpr int NS = ROLA ? E : 1;  // register overlap-add slots
     static constexpr int D = ROLA ? DT : 1;  // slots completed per frame (ROLA)
-    static constexpr bool GREG = PV_SYN_GREG && ROLA && (L <= 512 || (L == 1024 && DT == 4 && PV_SYN_GREG1024));
-    static constexpr bool RACC = QPOW2 && MODE != 1 && PV_REV_ACC;  // host: QPOW2 only for q <= 4096
+    static constexpr bool GREG = syn_gains_in_regs<L, DT>();
+    // revolution accumulator (synth_frame RACC; measured: synthesis -2.5 %); the host takes
+    // the QPOW2 kernels only for q <= 4096
+    static constexpr bool RACC = QPOW2 && MODE != 1;
 };
 
 // The frame loop of one wave's run: frames t0 .. t0 + F - 1 of channel c (frames >= nfr are
 // zero), unwrap state M / phprev initialised by the caller (M = the carry at t0, in the RACC
 // form when RACC).  On return acc holds the run's overlap tail (ROLA; slots D..NS-1) or
 // the ring does (DT = 0).
-// NTROW: spectrum rows loaded non-temporally.
 // LANEK: the unwrap constants are per-lane (e_k and (p j_k) mod q depend on k mod 64 only:
 // 64 a multiple of the hop divisor and q of 64 / hop divisor, checked by the host —
 // config 3 and 4): two registers (and bin L's j constant) instead of two LDS reads per bin
 // and frame.
-template <int L, int MODE, int DT, bool QPOW2, bool NTROW, bool LANEK = false>
+template <int L, int MODE, int DT, bool QPOW2, bool LANEK = false>
 __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, const float2 (&tw0)[Geo<L>::E],
                                         int lane, int w, int c, int t0, int nfr,
                                         int (&M)[Geo<L>::E + 1], float (&phprev)[Geo<L>::E + 1],
@@ -198,9 +174,8 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         }
     }
 
-    // unwrap constants of the lane's bins in registers for the whole run (ROLA kernels
-    // have VGPRs to spare below their LDS-bound occupancy)
-    constexpr bool KREG = (ROLA && MODE == 0 && PV_SYN_KREG) || (LANEK && MODE != 1);  // (MODE 2 would spill)
+    // unwrap constants of the lane's bins in registers for the whole run (per-lane kernels)
+    constexpr bool KREG = LANEK && MODE != 1;
     float ekr[E + 1];
     unsigned jkr[E + 1];
     if constexpr (LANEK && MODE != 1) {
@@ -218,9 +193,10 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     const PhaseMap pmap{p.rho * kInv2Pi, (unsigned)p.q, (unsigned)p.p_mod, p.q_pow2, p.inv_q,
                         (float)p.p_mod * p.inv_q, p.rho < 1.0f ? 1 : 0};
     const SynLds stb{sc.twl, sc.twsl, sc.ekl, sc.jkl, sc.srcl};
-    // L = 1024: the pre-step's split twiddles of the lane's bins in registers for the run
-    // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy)
-    using TwS = typename std::conditional<((L == 1024 || (L == 512 && PV_SYN_TWREG512 && LANEK)) && ROLA && PV_SYN_TWREG), TwReg<E>, NoTwReg>::type;
+    // the pre-step's split twiddles of the lane's bins in registers for the run: L = 1024
+    // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy) and the L = 512
+    // per-lane kernels (within their 3 waves/SIMD budget)
+    using TwS = typename std::conditional<((L == 1024 || (L == 512 && LANEK)) && ROLA), TwReg<E>, NoTwReg>::type;
     TwS twr;
     if constexpr (TwS::ON) {
 #pragma unroll
@@ -232,10 +208,10 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, NoHook, TwS>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile,
                                                                            lane, z, ekr, jkr, NoHook{}, twr);
     };
-    [[maybe_unused]] auto synth_h = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hook) {
-        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, std::decay_t<decltype(hook)>, TwS>(
-            sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hook, twr);
+    // PV_SPEC_PACKED rows: lane 0 finds bins 0 and L in slot 0 (the row has no slot L)
+    const bool packed = p.packed != 0;
+    auto unpack = [&](float2 (&sv)[E + 1]) {
+        if (packed && lane == 0) unpack_real_bins(sv[0], sv[0], sv[E]);
     };
     // ROLA: register z[idx] = samples 2 (lane + 64 cr) + {0,1}; REF_COMPAT's half swap
     // moves raw slot cr to OLA slot cr + E/2 (mod E)
@@ -258,11 +234,8 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         for (int d = 0; d < D; ++d) {
             const long long gp = pb + 128 * d;
             if (FAST || (p.out_aligned && gp + 1 < p.out_len)) {
-#if PV_NT_OUT
+                // non-temporal output stores: -0.5 %
                 __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
-#else
-                *reinterpret_cast<float2*>(outc + gp) = acc[d];
-#endif
             } else {
                 if (gp < p.out_len) outc[gp] = acc[d].x;
                 if (gp + 1 < p.out_len) outc[gp + 1] = acc[d].y;
@@ -281,61 +254,44 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
         // alternate (F is even), so no register copies carry a row across trips.
         auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
-#if PV_SYN_1BUF
-        // one row buffer: row u+1 is loaded into it once frame u's phase stage has
-        // consumed it (synth_frame hook), then the pre-step, FFT and overlap-add run
-        // while it is in flight: 18 VGPRs fewer than two buffers
-        f2v row[E + 1];
-        gload_row<E, NTROW>(row, rowp(0) + lane, rowp(0) + L);
-        vm_wait<0>(row);
-        for (int u = 0; u < p.F; ++u) {
-            float2 sv[E + 1];
-#pragma unroll
-            for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
-            float2 z[E];
-            synth_h(u, t0 + u, sv, z, [&] { gload_row<E, NTROW>(row, rowp(u + 1) + lane, rowp(u + 1) + L); });
-            ola_regs(z);
-            flush_regs(u, std::true_type{});  // exactly D stores
-            vm_wait<D>(row);
-        }
-#else
         auto step = [&](int u, const f2v (&row)[E + 1]) {
             float2 sv[E + 1];
 #pragma unroll
             for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
+            unpack(sv);
             float2 z[E];
             synth(u, t0 + u, sv, z);
             ola_regs(z);
             flush_regs(u, std::true_type{});  // exactly D stores
         };
+        // (packed rows: no bin-L load; vmcnt(D) still waits for every row load)
         f2v ra[E + 1], rb[E + 1];
-        gload_row<E, NTROW>(ra, rowp(0) + lane, rowp(0) + L);
+        gload_row<E>(ra, rowp(0) + lane, rowp(0) + L, !packed);
         vm_wait<0>(ra);
         for (int u = 0; u < p.F; u += 2) {
-            gload_row<E, NTROW>(rb, rowp(u + 1) + lane, rowp(u + 1) + L);
+            gload_row<E>(rb, rowp(u + 1) + lane, rowp(u + 1) + L, !packed);
             step(u, ra);
             vm_wait<D>(rb);
-            gload_row<E, NTROW>(ra, rowp(u + 2) + lane, rowp(u + 2) + L);
+            gload_row<E>(ra, rowp(u + 2) + lane, rowp(u + 2) + L, !packed);
             step(u + 1, rb);
             vm_wait<D>(ra);
         }
-#endif
     } else {
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
-        if (nfr > 0) {
-            const float2* srow = specc + (long long)t0 * p.spec_stride;
-            PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-        }
+        auto load_row = [&](const float2* srow) {
+            PV_FOR_BINS(E, lane, {
+                if (i < E || !packed) sv[i] = srow[k];
+            })
+            unpack(sv);
+        };
+        if (nfr > 0) load_row(specc + (long long)t0 * p.spec_stride);
         for (int u = 0; u < p.F; ++u) {
             const int t = t0 + u;
             if (u < nfr) {
                 float2 cur[E + 1];
 #pragma unroll
                 for (int i = 0; i <= E; ++i) cur[i] = sv[i];
-                if (u + 1 < nfr) {
-                    const float2* srow = specc + (long long)(t + 1) * p.spec_stride;
-                    PV_FOR_BINS(E, lane, { sv[i] = srow[k]; })
-                }
+                if (u + 1 < nfr) load_row(specc + (long long)(t + 1) * p.spec_stride);
                 float2 z[E];
                 synth(u, t, cur, z);
                 if constexpr (ROLA) {

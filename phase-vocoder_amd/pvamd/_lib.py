@@ -15,6 +15,8 @@ PV_OK, PV_ERR_ARG, PV_ERR_UNSUPPORTED, PV_ERR_HIP, PV_ERR_NOMEM = range(5)
 PV_TIME_SHIFT, PV_PITCH_SHIFT = ord("t"), ord("p")
 PV_MODE_REF_COMPAT, PV_MODE_STANDARD = 0, 1
 PV_WINDOW_DEFAULT, PV_WINDOW_HAMMING_REF, PV_WINDOW_HANN_REF = 0, 1, 2
+PV_SPEC_NATURAL, PV_SPEC_PACKED = 0, 1
+ABI_VERSION = 4  # PV_ABI_VERSION of include/pv.h (pv_config / pv_info lead with it)
 
 
 class PVError(RuntimeError):
@@ -24,19 +26,34 @@ class PVError(RuntimeError):
 
 
 class pv_config(ctypes.Structure):
-    _fields_ = [("n_samps", ctypes.c_int), ("hop_div", ctypes.c_int), ("effect", ctypes.c_int),
+    _fields_ = [("abi_version", ctypes.c_int), ("n_samps", ctypes.c_int), ("hop_div", ctypes.c_int), ("effect", ctypes.c_int),
                 ("scale", ctypes.c_float), ("mode", ctypes.c_int), ("max_channels", ctypes.c_int),
                 ("max_frames", ctypes.c_int), ("device", ctypes.c_int), ("window", ctypes.c_int),
-                ("nan_faithful", ctypes.c_int)]
+                ("nan_faithful", ctypes.c_int), ("spec_layout", ctypes.c_int)]
 
 
 class pv_info(ctypes.Structure):
-    _fields_ = [("n_samps", ctypes.c_int), ("hop", ctypes.c_int), ("out_hop", ctypes.c_int),
+    _fields_ = [("abi_version", ctypes.c_int), ("n_samps", ctypes.c_int), ("hop", ctypes.c_int), ("out_hop", ctypes.c_int),
                 ("spec_bins", ctypes.c_int), ("spec_stride", ctypes.c_int),
                 ("frames_per_run", ctypes.c_int), ("mode", ctypes.c_int), ("effect", ctypes.c_int),
                 ("scale", ctypes.c_float), ("single_launch", ctypes.c_int),
                 ("single_launch_frames", ctypes.c_int),
-                ("lane_constants", ctypes.c_int)]
+                ("lane_constants", ctypes.c_int), ("spec_layout", ctypes.c_int)]
+
+
+def config(n_samps, hop_div, effect, scale, mode, max_channels, max_frames, device=0, window=PV_WINDOW_DEFAULT,
+           nan_faithful=0, spec_layout=PV_SPEC_NATURAL) -> pv_config:
+    """A pv_config for this ABI (abi_version filled in)."""
+    return pv_config(ABI_VERSION, int(n_samps), int(hop_div), int(effect), float(scale), int(mode),
+                     int(max_channels), int(max_frames), int(device), int(window), int(nan_faithful),
+                     int(spec_layout))
+
+
+def new_info() -> pv_info:
+    """A pv_info for pv_get_info (abi_version filled in)."""
+    i = pv_info()
+    i.abi_version = ABI_VERSION
+    return i
 
 
 _lib = None
@@ -45,7 +62,8 @@ _lib = None
 def declared_symbols() -> list[str]:
     """Function names declared in include/pv.h (the ABI contract)."""
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(pv_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(m.group(2) for m in re.finditer(r"^\s*((?:[\w\s\*]+?))\b(pv_\w+)\s*\(", txt, flags=re.M)
+                      if "static" not in m.group(1)))  # static inline helpers are not exported
 
 
 def lib():

@@ -14,8 +14,8 @@ class Harmonizer:
                  max_frames: int = 4096, device: int = 0):
         self.ratios = [float(r) for r in ratios]
         K = len(self.ratios)
-        cfg = _lib.pv_config(int(samples), int(hop), _lib.PV_PITCH_SHIFT, 1.0, _lib.PV_MODE_STANDARD,
-                             int(max_channels), int(max_frames), int(device))
+        cfg = _lib.config(samples, hop, _lib.PV_PITCH_SHIFT, 1.0, _lib.PV_MODE_STANDARD, max_channels,
+                          max_frames, device)
         arr = (ctypes.c_float * K)(*self.ratios)
         h = ctypes.c_void_p()
         self._L = _lib.lib()

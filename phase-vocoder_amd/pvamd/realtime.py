@@ -21,8 +21,7 @@ class RealTimeVocoder:
     def __init__(self, samples: int, effect: str = PITCH_SHIFT, scaleFactor: float = 1.0,
                  hop: int = 4, *, channels: int = 1, device: int = 0):
         eff = effect if isinstance(effect, int) else ord(effect)
-        cfg = _lib.pv_config(int(samples), int(hop), eff, float(scaleFactor), _lib.PV_MODE_STANDARD,
-                             int(channels), 1, int(device))
+        cfg = _lib.config(samples, hop, eff, scaleFactor, _lib.PV_MODE_STANDARD, channels, 1, device)
         self._L = _lib.lib()
         h = ctypes.c_void_p()
         _lib.check(self._L.pv_rt_create(ctypes.byref(cfg), int(channels), ctypes.byref(h)), "pv_rt_create")

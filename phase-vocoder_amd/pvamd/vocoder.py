@@ -42,22 +42,24 @@ class PhaseVocoder:
     def __init__(self, samples: int, effect: str = TIME_SHIFT, scaleFactor: float = 1.0,
                  hop: int = 2, *, mode: str = REF_COMPAT, max_channels: int = 1,
                  max_frames: int = 4096, device: int = 0, exit_on_error: bool = False,
-                 window: int = _lib.PV_WINDOW_DEFAULT, nan_faithful: bool = False):
+                 window: int = _lib.PV_WINDOW_DEFAULT, nan_faithful: bool = False,
+                 spec_layout: int = _lib.PV_SPEC_NATURAL):
         """window: PV_WINDOW_DEFAULT (the mode's), PV_WINDOW_HAMMING_REF or
         PV_WINDOW_HANN_REF (the 1-argument constructor's, phaseVocoder.h:64-66; see
-        `single_arg`); nan_faithful: REF_COMPAT atanf(0/0) = NaN (kernel.cu:101-109)."""
+        `single_arg`); nan_faithful: REF_COMPAT atanf(0/0) = NaN (kernel.cu:101-109);
+        spec_layout: PV_SPEC_NATURAL or PV_SPEC_PACKED (STANDARD: bin N/2 folded into slot 0,
+        see `unpack_spec`)."""
         self.exit_on_error = exit_on_error
         eff = effect if isinstance(effect, int) else ord(effect)
         m = PV_MODE_REF_COMPAT if mode == REF_COMPAT else PV_MODE_STANDARD
-        cfg = _lib.pv_config(int(samples), int(hop), eff, float(scaleFactor), m,
-                             int(max_channels), int(max_frames), int(device), int(window),
-                             1 if nan_faithful else 0)
+        cfg = _lib.config(samples, hop, eff, scaleFactor, m, max_channels, max_frames, device, window,
+                          1 if nan_faithful else 0, spec_layout)
         self.window = int(window)
         h = ctypes.c_void_p()
         self._L = _lib.lib()
         self._call(self._L.pv_create(ctypes.byref(cfg), ctypes.byref(h)), "pv_create")
         self._h = h
-        info = _lib.pv_info()
+        info = _lib.new_info()
         self._call(self._L.pv_get_info(self._h, ctypes.byref(info)), "pv_get_info")
         self.info = info
         self.device = int(device)
@@ -76,6 +78,7 @@ class PhaseVocoder:
         self.single_launch = info.single_launch
         self.single_launch_frames = info.single_launch_frames
         self.lane_constants = info.lane_constants
+        self.spec_layout = info.spec_layout
 
     @classmethod
     def single_arg(cls, samples: int, **kw):
@@ -139,6 +142,25 @@ class PhaseVocoder:
         torch = _torch()
         return torch.zeros((channels, frames, self.spec_stride, 2), dtype=torch.float32,
                            device=f"cuda:{self.device}")
+
+    def unpack_spec(self, spec):
+        """Spectrum rows of this handle -> natural {mag, phase} bins 0 .. N/2, as a
+        [..., N/2 + 1, 2] float32 tensor (a copy).  PV_SPEC_PACKED rows carry bins 0 and N/2
+        in slot 0 as sign-coded magnitudes (include/pv.h pv_unpack_bins): exact."""
+        torch = _torch()
+        B = self.nSamps // 2 + 1
+        if self.spec_layout != _lib.PV_SPEC_PACKED:
+            return spec[..., :B, :].clone()
+        L = self.nSamps // 2
+        out = torch.empty(spec.shape[:-2] + (B, 2), dtype=spec.dtype, device=spec.device)
+        out[..., 1:L, :] = spec[..., 1:L, :]
+        s0 = spec[..., 0, :]
+        pi = torch.tensor(float(np.float32(np.pi)), dtype=spec.dtype, device=spec.device)
+        zero = torch.zeros((), dtype=spec.dtype, device=spec.device)
+        for dst, src in ((0, s0[..., 0]), (L, s0[..., 1])):
+            out[..., dst, 0] = src.abs()
+            out[..., dst, 1] = torch.where(torch.signbit(src), pi, zero)
+        return out
 
     def alloc_out(self, channels: int, frames: int):
         torch = _torch()

@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.pv_abi_version() == 3
+    assert L.pv_abi_version() == _lib.ABI_VERSION == 4
     assert L.pv_status_string(0) == b"PV_OK"
     assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
 
@@ -51,13 +51,13 @@ def test_frame_count_is_main_cpp_loop():
 def test_create_rejects_bad_configs_without_touching_gpu():
     L = _lib.lib()
     h = ctypes.c_void_p()
-    for cfg in (_lib.pv_config(1000, 4, ord("t"), 1.0, 1, 1, 10, 0),   # N not a power of 2
-                _lib.pv_config(1024, 0, ord("t"), 1.0, 1, 1, 10, 0),   # hop_div 0
-                _lib.pv_config(1024, 4, ord("x"), 1.0, 1, 1, 10, 0),   # bad effect
-                _lib.pv_config(1024, 4, ord("t"), -1.0, 1, 1, 10, 0),  # bad scale
-                _lib.pv_config(1024, 4, ord("p"), 2.0, 0, 1, 10, 0),   # compat has no pitch
-                _lib.pv_config(1024, 4, ord("t"), 1.0, 0, 1, 10, 0, 7),  # unknown window
-                _lib.pv_config(1024, 4, ord("t"), 1.0, 1, 1, 10, 0, 2)):  # STANDARD: Hann only
+    for cfg in (_lib.config(1000, 4, ord("t"), 1.0, 1, 1, 10, 0),   # N not a power of 2
+                _lib.config(1024, 0, ord("t"), 1.0, 1, 1, 10, 0),   # hop_div 0
+                _lib.config(1024, 4, ord("x"), 1.0, 1, 1, 10, 0),   # bad effect
+                _lib.config(1024, 4, ord("t"), -1.0, 1, 1, 10, 0),  # bad scale
+                _lib.config(1024, 4, ord("p"), 2.0, 0, 1, 10, 0),   # compat has no pitch
+                _lib.config(1024, 4, ord("t"), 1.0, 0, 1, 10, 0, 7),  # unknown window
+                _lib.config(1024, 4, ord("t"), 1.0, 1, 1, 10, 0, 2)):  # STANDARD: Hann only
         st = L.pv_create(ctypes.byref(cfg), ctypes.byref(h))
         assert st in (_lib.PV_ERR_ARG, _lib.PV_ERR_UNSUPPORTED)
         assert len(L.pv_last_error()) > 0
@@ -107,3 +107,30 @@ def test_prefetch_kernels_have_no_spills():
             checked += 1
             assert info.get("VGPRs Spill") == "0" and info.get("AGPRs") == "0", (name, info)
     assert checked >= 4 + 3 * 3 * 3
+
+
+def test_create_rejects_a_config_built_against_another_header():
+    """pv_config / pv_info lead with abi_version: a caller compiled against an
+    older pv.h is refused with PV_ERR_ARG instead of having its struct misread."""
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    cfg = _lib.config(1024, 4, ord("t"), 1.0, 1, 1, 10, 0)
+    for bad in (3, 0, 1024):  # an ABI-3 caller's first field is n_samps
+        cfg.abi_version = bad
+        assert L.pv_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.PV_ERR_ARG
+        assert b"abi_version" in L.pv_last_error()
+        assert not h.value
+
+
+def test_create_rejects_bad_spec_layouts():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    for cfg in (_lib.config(1024, 4, ord("t"), 1.0, 1, 1, 10, 0, spec_layout=2),     # unknown
+                _lib.config(1024, 4, ord("t"), 1.0, 0, 1, 10, 0, spec_layout=1)):    # REF_COMPAT
+        assert L.pv_create(ctypes.byref(cfg), ctypes.byref(h)) != _lib.PV_OK
+        assert not h.value
+
+
+def test_static_inline_helpers_are_not_abi_symbols():
+    assert "pv_unpack_bins" not in _lib.declared_symbols()
+    assert "pv_process" in _lib.declared_symbols()

@@ -123,7 +123,7 @@ def test_rt_rejects_ref_compat_and_bad_sizes(cuda):
     from pvamd import PVError
     from pvamd import _lib
     import ctypes
-    cfg = _lib.pv_config(1024, 4, ord("t"), 1.0, _lib.PV_MODE_REF_COMPAT, 1, 1, 0)
+    cfg = _lib.config(1024, 4, ord("t"), 1.0, _lib.PV_MODE_REF_COMPAT, 1, 1, 0)
     h = ctypes.c_void_p()
     assert _lib.lib().pv_rt_create(ctypes.byref(cfg), 1, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
     with pytest.raises(PVError):
