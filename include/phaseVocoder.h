@@ -16,12 +16,25 @@
 //                                                (phaseVocoder.h:79-116)
 // The batched handle `handle` (pv_process etc.) is created with the same window.
 //
+// Real time (main.cpp:45-59 `callback`, RT block): the callback memcpys one RtAudio buffer
+// into `curr_input` and calls analysis(); the reference declares analysis() and
+// analysis(float*) (phaseVocoder.h:131-132) but only sketches them (phaseVocoder.cpp:6-19:
+// pv_analysis_RT of the new samples on a round-robin stream).  Here they push the buffer's
+// nSamps samples (main.cpp:85: bufferSize = nSamps) through libpv's real-time stream
+// (pv_rt_push: input history, phases, unwrap counts and the overlap accumulator stay on the
+// device between callbacks): the spectra of the buffer's nSamps/hopSize frames land in
+// `curr_mag_phase`, the buffer's nSamps/hopSize * outHopSize emitted samples in
+// `prev_output`.  The stream runs the STANDARD pipeline (the phase vocoder the reference's
+// real-time design plans, README.md:46-50, with the object's effect and scale).
+//
 // What differs by construction: no cuFFT plans (`plan`, `ifft` are 0), the
-// managed-memory attach calls do not exist, and STANDARD mode (an extension: the
-// textbook vocoder the reference never implemented) runs on `handle` directly.
+// managed-memory attach calls do not exist, the real-time buffers are allocated by both
+// constructors (sized for one callback), and STANDARD mode (an extension: the textbook
+// vocoder the reference never implemented) runs on `handle` directly.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -69,18 +82,21 @@ class PhaseVocoder {
     // phaseVocoder.h:46-78: hop = samples/2, timeScale 1, periodic Hann
     // imp[i] = 0.5f*(1.f - cosf(2.f*M_PI*i/samples)); the real-time buffers are allocated
     explicit PhaseVocoder(int samples, int max_channels = 1, int max_frames = PV_DEFAULT_MAX_FRAMES,
-                          int device = 0) {
-        init(samples, TIME_SHIFT, 1.0f, 2, PV_MODE_REF_COMPAT, PV_WINDOW_HANN_REF, max_channels, max_frames,
-             device);
+                          int device = 0)
+        : PhaseVocoder(samples, PV_MODE_REF_COMPAT, max_channels, max_frames, device) {}
+
+    // PhaseVocoder(int samples) with the mode chosen: REF_COMPAT is the 1-argument
+    // constructor; STANDARD takes its geometry (hop N/2, time scale 1) with the STANDARD
+    // periodic Hann window.  (Keeps `PhaseVocoder(N, PV_MODE_STANDARD)` from converting the
+    // enum to the 1-argument constructor's max_channels.)
+    PhaseVocoder(int samples, pv_mode mode, int max_channels = 1, int max_frames = PV_DEFAULT_MAX_FRAMES,
+                 int device = 0) {
+        init(samples, TIME_SHIFT, 1.0f, 2, mode, mode == PV_MODE_REF_COMPAT ? PV_WINDOW_HANN_REF : PV_WINDOW_DEFAULT,
+             max_channels, max_frames, device);
         std::vector<float> w(2 * (size_t)samples);  // imp1: 2N entries (the reference writes
         for (int i = 0; i < 2 * samples; ++i)          // 2N into an N-float buffer)
             w[i] = 0.5f * (1.f - cosf((float)(2.0 * M_PI * (double)i / (double)samples)));
         imp1 = managed_copy(w.data(), 2 * (size_t)samples, "Malloc imp1 error");
-        prev_mag_phase = (float2*)managed_zero(sizeof(float) * 2 * samples, "Malloc prev_mag_phase error");
-        prev_input = (float*)managed_zero(sizeof(float) * samples, "Malloc prev_input");
-        prev_output = (float*)managed_zero(sizeof(float) * samples, "Malloc prev_output");
-        curr_mag_phase = (float2*)managed_zero(sizeof(float) * samples, "Malloc curr_mag_phase");
-        curr_input = (float*)managed_zero(sizeof(float) * samples, "Malloc curr_input");
     }
 
     // phaseVocoder.h:79-116: hop = samples / hop (the 4th argument is a divisor), symmetric
@@ -104,6 +120,7 @@ class PhaseVocoder {
             if (b) (void)hipFree(b);
         for (auto& s : streams)
             if (s) (void)hipStreamDestroy(s);
+        pv_rt_destroy(rt_);
         pv_destroy(handle);
     }
 
@@ -159,12 +176,39 @@ class PhaseVocoder {
             resynthesis_CUFFT(backFrame, frontFrame, output);
         }
     }
-    // phaseVocoder.cpp:77-78 declares the processing hook and leaves its body empty (the
-    // reference's planned processing stage, README.md:22-23).  Here the hook runs on the
-    // analysed spectrum `magFreq`, then the frame is resynthesised like resynthesis_CUFFT.
+    // phaseVocoder.cpp:77-78: the processing-hook overload has an empty body in the
+    // reference (its planned processing stage, README.md:22-23); it does nothing here either
+    // (neither the hook nor a resynthesis runs)
     void resynthesis(float* backFrame, float2* magFreq, float* output, void (*processing)()) {
-        if (processing) processing();
-        resynthesis_CUFFT(backFrame, magFreq, output);
+        (void)backFrame;
+        (void)magFreq;
+        (void)output;
+        (void)processing;
+    }
+
+    // phaseVocoder.h:132, main.cpp:53-54: one RtAudio buffer of nSamps samples (host-written
+    // managed or device memory) through the real-time stream; emitted samples ->
+    // prev_output (rtOutputSamples() of them), analysed rows -> curr_mag_phase
+    // (rtFrames() rows of specStride() {mag, phase} float2 each).  Synchronous.
+    void analysis(float* input) {
+        ensure_rt();
+        sync();
+        const int fr = rtFrames();
+        checkCUDAErrori(pv_rt_push(rt_, input, nSamps, fr, prev_output, (long long)fr * outHopSize,
+                                   (pv_float2*)curr_mag_phase, (long long)fr * rt_spec_stride_, nullptr),
+                        "pv_analysis_RT", __LINE__);
+        sync();
+    }
+    // phaseVocoder.h:131: the callback's form, on curr_input (main.cpp:53 memcpys into it)
+    void analysis() { analysis(curr_input); }
+    int rtFrames() const { return hopSize > 0 ? nSamps / hopSize : 0; }  // frames per buffer
+    int rtOutputSamples() const { return rtFrames() * outHopSize; }    // emitted per buffer
+    int rtSpecStride() const { return rt_spec_stride_; }               // float2 per curr_mag_phase row
+    // start a new real-time stream (zero history, phases, overlap accumulator)
+    void rtReset() {
+        ensure_rt();
+        checkCUDAErrori(pv_rt_reset(rt_, nullptr), "pv_rt_reset", __LINE__);
+        sync();
     }
 
     // phaseVocoder.cpp:20-23 -> kernel.cu:289-298: window, shift, unshift, window, OLA
@@ -178,6 +222,37 @@ class PhaseVocoder {
    private:
     int spec_stride_ = 0;
     pv_mode mode_ = PV_MODE_REF_COMPAT;
+    Effect effect_ = TIME_SHIFT;
+    float scale_ = 1.0f;
+    int device_ = 0;
+    pv_rt* rt_ = nullptr;  // real-time stream behind analysis() (created on first use)
+    int rt_spec_stride_ = 0;
+
+    void ensure_rt() {
+        if (rt_) return;
+        pv_config cfg{};
+        cfg.abi_version = PV_ABI_VERSION;
+        cfg.n_samps = nSamps;
+        cfg.hop_div = nSamps / hopSize;
+        cfg.effect = (int)effect_;
+        cfg.scale = scale_;
+        cfg.mode = PV_MODE_STANDARD;
+        cfg.max_channels = 1;
+        cfg.max_frames = rtFrames();
+        cfg.device = device_;
+        checkCUDAErrori(pv_rt_create(&cfg, 1, &rt_), "pv_rt_create", __LINE__);
+    }
+    void alloc_rt_buffers() {
+        // sized for one callback of nSamps samples (the reference's sizes are per frame)
+        const size_t N = (size_t)nSamps, fr = (size_t)rtFrames();
+        rt_spec_stride_ = (int)(((N / 2 + 1) + 7) & ~(size_t)7);
+        const size_t out_n = std::max(N, fr * (size_t)outHopSize);
+        prev_mag_phase = (float2*)managed_zero(sizeof(float2) * fr * rt_spec_stride_, "Malloc prev_mag_phase error");
+        prev_input = (float*)managed_zero(sizeof(float) * N, "Malloc prev_input");
+        prev_output = (float*)managed_zero(sizeof(float) * out_n, "Malloc prev_output");
+        curr_mag_phase = (float2*)managed_zero(sizeof(float2) * fr * rt_spec_stride_, "Malloc curr_mag_phase");
+        curr_input = (float*)managed_zero(sizeof(float) * N, "Malloc curr_input");
+    }
 
     static void sync() {
         if (hipStreamSynchronize(nullptr) != hipSuccess)
@@ -220,6 +295,9 @@ class PhaseVocoder {
         timeScale = (e == TIME_SHIFT) ? scaleFactor : 1.0f;
         spec_stride_ = info.spec_stride;
         mode_ = mode;
+        effect_ = e;
+        scale_ = scaleFactor;
+        device_ = device;
         // imp: the constructor's recipe (float argument, float cos as in the reference)
         std::vector<float> w(samples);
         if (mode == PV_MODE_STANDARD) {
@@ -235,5 +313,6 @@ class PhaseVocoder {
         imp = managed_copy(w.data(), samples, "Malloc imp error");
         for (auto& s : streams)  // phaseVocoder.h:112-114
             if (hipStreamCreate(&s) != hipSuccess) checkCUDAErrori(PV_ERR_HIP, "stream create", __LINE__);
+        alloc_rt_buffers();
     }
 };

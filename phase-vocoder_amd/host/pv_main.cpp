@@ -13,6 +13,12 @@
 //     --nan-faithful                     atanf(0/0) = NaN phases as the reference (kernel.cu:101-109)
 //     --timer                            print CudaPhase::timer() per call (main.cpp:238-241, 275-278)
 //     --dump-f32 <file>                  raw float32 of the emitted channel-0 samples
+//     --rt                               main.cpp's RT block instead of the offline loop: the
+//                                        RtAudio `callback` (main.cpp:45-59) is called on
+//                                        successive nSamps-sample buffers of channel 0
+//                                        (main.cpp:85 bufferSize = nSamps); each memcpys into
+//                                        curr_input and runs analysis(); the buffer's emitted
+//                                        samples (prev_output) are the output stream
 //
 // The per-frame REF_COMPAT calls go PhaseVocoder -> CudaPhase (include/kernel.h) with the
 // object's window, as phaseVocoder.cpp -> kernel.cu do.
@@ -43,12 +49,26 @@
         }                                                                             \
     } while (0)
 
+// main.cpp:45-59 (RT): the RtAudio callback, on this build's drop-in.  The output buffer
+// receives the buffer's emitted samples (the reference leaves its resynthesis commented
+// out, main.cpp:55).
+static int callback(void* outputBuffer, void* inputBuffer, unsigned int nBufferFrames, double streamTime,
+                    unsigned int status, void* UserData) {
+    (void)streamTime;
+    PhaseVocoder* pv = (PhaseVocoder*)UserData;
+    if (status) std::printf("Stream underflow detected!\n");
+    std::memcpy(pv->curr_input, inputBuffer, sizeof(float) * nBufferFrames);  // main.cpp:53
+    pv->analysis();                                                            // main.cpp:54
+    std::memcpy(outputBuffer, pv->prev_output, sizeof(float) * pv->rtOutputSamples());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     std::string in = "testtones/1000sine.wav", out = "out.wav", dump;
     Effect effect = TIME_SHIFT;
     int N = 256, hopdiv = 2;
     float scale = 1.0f;
-    bool batched = false, single_arg = false, show_timer = false;
+    bool batched = false, single_arg = false, show_timer = false, rt = false;
     double ana_ms = 0.0, syn_ms = 0.0;
     pv_mode mode = PV_MODE_REF_COMPAT;
     std::vector<std::string> pos;
@@ -63,6 +83,7 @@ int main(int argc, char** argv) {
         else if (a == "--nan-faithful") CudaPhase::set_nan_faithful(true);
         else if (a == "--timer") show_timer = true;
         else if (a == "--dump-f32" && i + 1 < argc) dump = argv[++i];
+        else if (a == "--rt") rt = true;
         else pos.push_back(a);
     }
     if (pos.size() >= 1) in = pos[0];                                    // main.cpp:69-81
@@ -105,7 +126,21 @@ int main(int argc, char** argv) {
                            sizeof(float) * numSamples, hipMemcpyHostToDevice));
     std::vector<float> emitted;
 
-    if (batched) {
+    if (rt) {
+        // main.cpp:84-101 + RT block: buffers of bufferSize = nSamps frames of channel 0
+        const unsigned int bufferSize = phase.nSamps;
+        std::vector<float> inBuf(bufferSize), outBuf((size_t)std::max(phase.rtOutputSamples(), 1));
+        std::printf("Real-time callbacks\n");
+        int outIndex = 0;
+        for (int i = 0; i + (int)bufferSize <= numSamples; i += bufferSize) {
+            std::memcpy(inBuf.data(), audio.samples[0].data() + i, sizeof(float) * bufferSize);
+            callback(outBuf.data(), inBuf.data(), bufferSize, (double)i / audio.sample_rate, 0, &phase);
+            for (int j = 0; j < phase.rtOutputSamples(); ++j, ++outIndex) {
+                if (outIndex < outLen) outFile[0][outIndex] = outFile[1][outIndex] = outBuf[j];
+                emitted.push_back(outBuf[j]);
+            }
+        }
+    } else if (batched) {
         const int S = phase.specStride();
         const long long olen = pv_output_length(phase.handle, frames);
         pv_float2* d_spec = nullptr;

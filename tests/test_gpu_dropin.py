@@ -253,3 +253,31 @@ def test_gpu_reproduces_reference_output_testout_wav(cuda, tmp_path, batched):
     assert np.abs(d).max() <= 1
     assert np.mean(d == 0) >= 0.999
     assert np.array_equal(s[0], s[1])
+
+
+@pytest.mark.parametrize("args,N,hop_div,effect,scale", [
+    ([], 256, 2, "t", 1.0),                                                  # main.cpp:84 geometry
+    (["--N", "1024", "--hopdiv", "4", "--scale", "0.5", "--mode", "std"], 1024, 4, "t", 0.5),
+    (["--single-arg", "--N", "512"], 512, 2, "t", 1.0),                     # PhaseVocoder(int)
+])
+def test_pv_main_rt_callback_stream(cuda, sine440, tmp_path, args, N, hop_div, effect, scale):
+    """main.cpp's RT block (main.cpp:45-59) on the drop-in: the RtAudio-shaped callback
+    memcpys each nSamps-sample buffer into curr_input and calls analysis()
+    (phaseVocoder.h:131-132); the buffers' emitted samples are the oracle's pipeline over the
+    stream prefixed with N - hop zeros (the real-time contract, include/pv.h)."""
+    path, x = sine440
+    x = x[:60000]
+    p2 = str(tmp_path / "in.wav")
+    write_pcm16(p2, x)
+    dump = str(tmp_path / "rt.f32")
+    r = subprocess.run([PV_MAIN, p2, effect, str(tmp_path / "rt.wav"), "--rt", "--dump-f32", dump] + args,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(dump, np.float32)
+    hop = N // hop_div
+    hs = int(scale * hop)
+    K = (len(x) // N) * (N // hop)  # frames of the whole buffers pushed
+    assert got.shape == (K * hs,)
+    xp = np.concatenate([np.zeros(N - hop, np.float32), x[:K * hop]])
+    ref = pvref.std_process(xp, N, hop_div, ord(effect), scale, frames=K)
+    assert rms(got, ref[:K * hs]) <= 1e-5
