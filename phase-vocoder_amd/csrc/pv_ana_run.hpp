@@ -20,7 +20,8 @@ template <int L>
 constexpr int ana_twl_n() { return ana_tws_min<L>() > 0 ? ana_tws_min<L>() : L; }
 
 // bins per batch of LDS reads + atan2 chains (measured with the bpermute split: 2 vs 3 ->
-// config-3 analysis -0.7 %, config 4 +-0.3 %; 4: +0.2 %)
+// config-3 analysis -0.7 %, config 4 +-0.3 %; 4: +0.2 %; with the packed atan2 of a pair,
+// 2 vs 4: -1 %)
 constexpr int kAnaChunk = 2;
 
 // LDS tables the analysis reads
@@ -89,13 +90,26 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             constexpr int p0 = decltype(ic)::value * CH;
             float2 X[CH];
             split_chunk_bp<L, CH, true, p0, PACKED>(z, twsl, lane, X);
+            // phases of the chunk's bins: pairs through the packed atan2
+            float phs[CH];
+            static_for<0, CH / 2>([&](auto jj) {
+                constexpr int j = 2 * decltype(jj)::value;
+                if constexpr (p0 + j + 1 <= E) {
+                    const f2v ph2 = atan2_pv2(X[j].y, X[j].x, X[j + 1].y, X[j + 1].x);
+                    phs[j] = ph2.x;
+                    phs[j + 1] = ph2.y;
+                } else if constexpr (p0 + j <= E) {
+                    phs[j] = atan2_pv(X[j].y, X[j].x);
+                }
+            });
+            if constexpr (CH % 2 == 1 && p0 + CH - 1 <= E) phs[CH - 1] = atan2_pv(X[CH - 1].y, X[CH - 1].x);
             static_for<0, CH>([&](auto cc) {
                 constexpr int c2 = decltype(cc)::value;
                 if constexpr (p0 + c2 <= E) {
                     constexpr int i = bin_at<E, PACKED>(p0 + c2);
                     const int k = (i == E) ? L : lane + 64 * i;
                     (void)k;
-                    const float ph = atan2_pv(X[c2].y, X[c2].x);
+                    const float ph = phs[c2];
                     if constexpr (!IS_HALO) {
                         // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
                         // the phase, which drives the unwrap decisions, stays bit-exact.  X

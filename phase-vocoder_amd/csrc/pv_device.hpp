@@ -220,6 +220,50 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     return __builtin_copysignf(rr, y);  // rr >= 0 here: the sign of y (v_bfi_b32)
 }
 
+// atan2_pv of two bins at once: the same operations on each half of a register pair, the
+// Newton steps and the polynomial as v_pk_fma_f32 / v_pk_mul_f32 (each half rounds exactly
+// like the scalar op, so both results are atan2_pv's bit for bit): 18 VALU fewer per pair.
+// The min/max, the seeds and the octant fix-ups stay scalar on the halves (no packed forms;
+// they read and write the pair's registers directly, no moves).
+__device__ __forceinline__ f2v atan2_pv2(float y0, float x0, float y1, float x1) {
+    f2v mx, mn, r;
+    float t0, t1, u0, u1;
+    asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(t0) : "v"(x0), "v"(y0), "s"(0x1p-126f));
+    asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(t1) : "v"(x1), "v"(y1), "s"(0x1p-126f));
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(u0) : "v"(x0), "v"(y0));
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(u1) : "v"(x1), "v"(y1));
+    mx = f2v{t0, t1};
+    mn = f2v{u0, u1};
+    r = f2v{__uint_as_float(0x7EF311C3u - __float_as_uint(t0)), __uint_as_float(0x7EF311C3u - __float_as_uint(t1))};
+    const f2v one = f2v{1.0f, 1.0f};
+    f2v e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    const f2v a = mn * r;
+    const f2v sq = a * a;
+    auto c = [](float v) { return f2v{v, v}; };
+    f2v p = c(-0x1.8ba68ap-10f);
+    p = __builtin_elementwise_fma(p, sq, c(0x1.398008p-7f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.d2ca58p-6f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.c2c9f4p-5f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.506f6cp-4f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.bd9028p-4f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.23c87ap-3f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.9986ecp-3f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.5554eep-2f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.000000p+0f));
+    const f2v rr = a * p;
+    float r0 = rr.x, r1 = rr.y;
+    if (__builtin_fabsf(y0) > __builtin_fabsf(x0)) r0 = kHalfPi - r0;
+    if (__builtin_fabsf(y1) > __builtin_fabsf(x1)) r1 = kHalfPi - r1;
+    if (x0 < 0.0f) r0 = kPi - r0;
+    if (x1 < 0.0f) r1 = kPi - r1;
+    return f2v{__builtin_copysignf(r0, y0), __builtin_copysignf(r1, y1)};
+}
+
 // sin/cos of 2 pi rev: the hardware v_sin_f32 / v_cos_f32 (inputs in revolutions,
 // quarter-rate transcendental; they reduce their input themselves over [-256, 256]
 // revolutions, and every caller passes |rev| < 4: output phases are carried reduced;

@@ -39,7 +39,7 @@ def _pair(N, hop_div, effect, scale, C, frames):
 def test_packed_process_bit_identical(cuda, N, hop_div, effect, scale):
     C, n = 3, 50000 + 777
     xs = np.stack([synth(n, 900 + c) for c in range(C)])
-    nat, pk = _pair(N, hop_div, effect, scale, C, 400)
+    nat, pk = _pair(N, hop_div, effect, scale, C, n // (N // hop_div) + 2)
     xd = to_dev(xs)
     out_n, spec_n = nat.process(xd)
     out_p, spec_p = pk.process(xd)
@@ -63,7 +63,7 @@ def test_packed_split_entry_points(cuda, N, hop_div, effect, scale):
     and N/2 from slot 0) equals the natural layout's output."""
     n = 40000
     x = synth(n, 5)
-    nat, pk = _pair(N, hop_div, effect, scale, 1, 200)
+    nat, pk = _pair(N, hop_div, effect, scale, 1, n // (N // hop_div) + 2)
     xd = to_dev(x)
     outs = []
     for pv in (nat, pk):
