@@ -87,35 +87,46 @@ def _pvref():
     return pvref
 
 
-def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False):
+def _oracle_batch(pvref, compat):
+    """The oracle's batched path: (x, N, hop_div, effect, scale, frames, threads) ->
+    (out, threads used).  REF_COMPAT: the fp64 restatement of kernel.cu / main.cpp."""
+    if compat:
+        return lambda x, N, hd, e, s, fr, th: pvref.compat_process_batch(x, N, hd, fr, th)
+    return pvref.std_process_batch
+
+
+def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, compat=False):
     """The CPU oracle (oracle/pvref.c, OpenMP over channels) timed on a bounded sample of
     the SAME host channels the GPU processes (x: [C, n] float32).  A single stream
     (single=True) has no channel parallelism and runs on one core."""
     pvref = _pvref()
+    batch = _oracle_batch(pvref, compat)
+    what = ("oracle/pvref.c REF_COMPAT fp64 restatement" if compat
+            else "oracle/pvref.c fp32-contract analysis + fp64 synthesis")
     threads, aff = cpu_share()
     C_all, n = x.shape
     frames = pvref.num_frames(n, N // hop_div)
     host = f"{threads} threads = this process's CPU share (affinity {aff}, machine {os.cpu_count()})"
     if single:
         t0 = time.perf_counter()
-        _, used = pvref.std_process_batch(x[:1], N, hop_div, effect, scale, frames, 1)
+        _, used = batch(x[:1], N, hop_div, effect, scale, frames, 1)
         dt = time.perf_counter() - t0
         return {"value": frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
                 "sample": f"the whole stream ({n} samples, {frames} frames) on 1 core, "
                           f"oracle/pvref.c, {dt:.1f} s wall"}
     k = min(threads, C_all)
     t0 = time.perf_counter()
-    _, used = pvref.std_process_batch(x[:k], N, hop_div, effect, scale, frames, threads)
+    _, used = batch(x[:k], N, hop_div, effect, scale, frames, threads)
     dt = time.perf_counter() - t0
     rate = k * frames / dt
     C = max(k, int(rate * target_s / frames) // threads * threads)
     C = min(C, C_all)
     t0 = time.perf_counter()
-    _, used = pvref.std_process_batch(x[:C], N, hop_div, effect, scale, frames, threads)
+    _, used = batch(x[:C], N, hop_div, effect, scale, frames, threads)
     dt = time.perf_counter() - t0
     return {"value": C * frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
             "sample": f"channels 0..{C - 1} of the GPU batch x {n} samples ({C * frames} frames), "
-                      f"oracle/pvref.c fp32-contract analysis + fp64 synthesis, {dt:.1f} s wall; "
+                      f"{what}, {dt:.1f} s wall; "
                       f"{host}"}
 
 
@@ -124,18 +135,20 @@ def check_channels(C, k=16):
     return sorted(set(int(round(v)) for v in np.linspace(0, C - 1, min(k, C))))
 
 
-def oracle_check(x, out_rows, idx, N, hop_div, effect, scale, frames, all_finite):
+def oracle_check(x, out_rows, idx, N, hop_div, effect, scale, frames, all_finite, compat=False):
     """RMS per sample of the GPU output against the oracle on the sampled channels of
     the timed batch (BASELINE.json metric: "RMS err vs CPU ref"; bar 1e-5)."""
     pvref = _pvref()
     threads, _ = cpu_share()
-    ref, _ = pvref.std_process_batch(x[idx], N, hop_div, effect, scale, frames, threads)
+    ref, _ = _oracle_batch(pvref, compat)(x[idx], N, hop_div, effect, scale, frames, threads)
     got = out_rows[:, :ref.shape[1]]
     rms = np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2, axis=1))
     return {"max": float(rms.max()), "mean": float(rms.mean()), "tol": 1e-5,
             "pass": bool(rms.max() <= 1e-5 and all_finite), "channels": idx,
             "all_finite": bool(all_finite),
-            "oracle": "oracle/pvref.c pvr_std_process_batch (fp32-contract analysis, fp64 synthesis)"}
+            "oracle": ("oracle/pvref.c pvr_compat_process_batch (fp64 restatement of kernel.cu / main.cpp)"
+                       if compat else
+                       "oracle/pvref.c pvr_std_process_batch (fp32-contract analysis, fp64 synthesis)")}
 
 
 def main():
@@ -154,10 +167,11 @@ def main():
                     help="STANDARD spectrum rows of the pv_process workspace (include/pv.h "
                          "pv_spec_layout): packed (default) folds the real bin N/2 into slot 0 "
                          "so every row store is whole 64-byte segments")
-    ap.add_argument("--workload", choices=["c3", "c2", "c4", "rt", "batch"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c2", "c4", "compat", "rt", "batch"], default="c3",
                     help="c3 (= batch): configs[2], the headline line (default); c2: configs[1] "
                          "single 60 s stream, pitch 2.0; c4: configs[3] per-GPU slice (1024 ch, "
-                         "N=2048 hop=512, pitch 1.5); rt: configs[4] real-time mode")
+                         "N=2048 hop=512, pitch 1.5); compat: the reference's own path (REF_COMPAT) "
+                         "at configs[2]'s size; rt: configs[4] real-time mode")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -197,7 +211,7 @@ def main():
     # the device the few collectives of the bench (timing, check) run on
     cdev = dev if backend == "nccl" else torch.device("cpu")
 
-    from pvamd import PITCH_SHIFT, PhaseVocoder, STANDARD, TIME_SHIFT
+    from pvamd import PITCH_SHIFT, REF_COMPAT, PhaseVocoder, STANDARD, TIME_SHIFT
     from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED
 
     wl = "c3" if args.workload == "batch" else args.workload
@@ -208,13 +222,20 @@ def main():
           "c2": (1024, 4, PITCH_SHIFT, 2.0, 60.0, 1,
                  "BASELINE configs[1]: single mono 44.1 kHz stream x 60 s, N=1024 hop=256, "
                  "PV_STANDARD pitch 2.0"),
+          "compat": (1024, 4, TIME_SHIFT, 1.0, args.seconds, args.channels,
+                     "the reference's active path (REF_COMPAT: kernel.cu:299-348 analysis to 2N "
+                     "{mag, atanf(Im/Re)} bins, kernel.cu:352-432 resynthesis, running OLA), "
+                     "1024 mono ch x 10 s per GPU, N=1024 hop=256"),
           "c4": (2048, 4, PITCH_SHIFT, 1.5, args.seconds, args.channels,
                  "BASELINE configs[3] per-GPU slice: 1024 mono ch x 10 s per GPU, N=2048 hop=512, "
                  "PV_STANDARD pitch 1.5 (8192 ch on 8 GPUs)")}
     N, hop_div, effect, scale, seconds, C, wl_desc = WL[wl]
     n = int(round(seconds * SR))
+    compat = wl == "compat"
+    if compat:
+        args.layout = "natural"  # REF_COMPAT rows: the 2N bins of kernel.cu:337
     layout = PV_SPEC_PACKED if args.layout == "packed" else PV_SPEC_NATURAL
-    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C,
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=REF_COMPAT if compat else STANDARD, max_channels=C,
                       max_frames=pv_frames(n, N // hop_div), device=local, spec_layout=layout)
     frames = pv.num_frames(n)
     tables = None
@@ -262,9 +283,13 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
     # Spectrum bytes per frame = the row the layout stores: 8 (N/2+1) natural,
     # 8 N/2 packed (bin N/2 rides in slot 0): the packed figure is the smaller, not inflated
+    # REF_COMPAT writes 2N bins per frame (kernel.cu:337) and its resynthesis reads the
+    # N/2+1 of them its size-N C2R uses (kernel.cu:363-368)
     hop_a, hop_s, B = N // hop_div, pv.outHopSize, pv.spec_bins
+    B_read = N // 2 + 1 if compat else B
     per_frame = {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
-                 "synthesis": 8 * B + 4 * hop_s,         # spectrum read + emitted output
+                 "compat_analysis": 4 * hop_a + 8 * B,
+                 "synthesis": 8 * B_read + 4 * hop_s,    # spectrum read + emitted output
                  "carry": 0, "runsum": 8 * B, "seam": 0,
                  # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
                  "fused": 4 * hop_a + 8 * B + 4 * hop_s}
@@ -311,7 +336,7 @@ def main():
         idx = check_channels(C)
         finite = bool(torch.isfinite(out).all().item())
         check = oracle_check(x_host, out[idx].cpu().numpy(), idx, N, hop_div, ord(effect), scale,
-                             frames, finite)
+                             frames, finite, compat=compat)
         if world > 1:  # worst rank
             t = torch.tensor([check["max"], check["mean"], 0.0 if check["pass"] else 1.0,
                               0.0 if finite else 1.0], dtype=torch.float64, device=cdev)
@@ -320,12 +345,12 @@ def main():
                          channels=f"{len(idx)} per rank (indices as rank 0's, rank-local)")
             check["pass"] = bool(t[2] == 0)
             check["all_finite"] = bool(t[3] == 0)
-    path_bytes = (4 * hop_a + 4 * hop_s + 2 * 8 * B) * C * frames * world * args.steps
+    path_bytes = (4 * hop_a + 4 * hop_s + 8 * B + 8 * B_read) * C * frames * world * args.steps
 
     cpu = None
     if rank == 0 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(x_host, N, hop_div, ord(effect), scale, single=(C == 1))
+            cpu = cpu_baseline(x_host, N, hop_div, ord(effect), scale, single=(C == 1), compat=compat)
         except Exception as e:  # reported, never fatal for the GPU number
             cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                    "sample": f"failed: {e}"}

@@ -436,6 +436,37 @@ int pvr_std_process_batch(const float* x, long ldx, long n, int C, int N, int ho
     return used;
 }
 
+int pvr_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
+                             int frames, float* out, long ldo, int threads) {
+    const int hop = N / hop_div;
+    const long out_len = (long)frames * hop + (N - hop);
+    int used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+        double* buf = (double*)malloc(sizeof(double) * (size_t)out_len);
+#pragma omp for schedule(dynamic, 1)
+        for (int ch = 0; ch < C; ++ch) {
+            pvr_compat_process(x + (size_t)ch * ldx, n, N, hop_div, frames, buf);
+            for (long i = 0; i < out_len; ++i) out[(size_t)ch * ldo + i] = (float)buf[i];
+        }
+        free(buf);
+    }
+#else
+    (void)threads;
+    double* buf = (double*)malloc(sizeof(double) * (size_t)out_len);
+    for (int ch = 0; ch < C; ++ch) {
+        pvr_compat_process(x + (size_t)ch * ldx, n, N, hop_div, frames, buf);
+        for (long i = 0; i < out_len; ++i) out[(size_t)ch * ldo + i] = (float)buf[i];
+    }
+    free(buf);
+#endif
+    return used;
+}
+
 /* ------------------------------------------------------------------ REF_COMPAT */
 
 void pvr_compat_analysis_frame(const float* frame, int N, const float* win, pvr_c64* b,

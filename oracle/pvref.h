@@ -95,6 +95,9 @@ void pvr_fft_c64(pvr_c64* data, int L, int inverse);     /* unnormalised radix-2
 int pvr_std_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
                           int effect, float scale, int frames, float* out, long ldo,
                           int threads);
+/* REF_COMPAT (pvr_compat_process, the 4-argument constructor's Hamming) per channel */
+int pvr_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
+                             int frames, float* out, long ldo, int threads);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,9 @@ def lib():
         L.pvr_std_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                             c_float, c_int, _f32p, c_long, c_int]
         L.pvr_std_process_batch.restype = c_int
+        L.pvr_compat_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
+                                               _f32p, c_long, c_int]
+        L.pvr_compat_process_batch.restype = c_int
         _lib = L
     return _lib
 
@@ -188,6 +191,20 @@ def std_process_batch(x, N, hop_div, effect, scale, frames=None, threads=0):
     out = np.zeros((C, olen), np.float32)
     used = lib().pvr_std_process_batch(x, n, n, C, N, hop_div, effect, float(scale), frames,
                                        out, olen, int(threads))
+    return out, used
+
+
+def compat_process_batch(x, N, hop_div, frames=None, threads=0):
+    """REF_COMPAT per channel (x: [C, n] float32, OpenMP over channels).
+    Returns (out [C, len] float32, threads_used)."""
+    x = _c32(x)
+    C, n = x.shape
+    hop = N // hop_div
+    if frames is None:
+        frames = num_frames(n, hop)
+    olen = frames * hop + (N - hop)
+    out = np.zeros((C, olen), np.float32)
+    used = lib().pvr_compat_process_batch(x, n, n, C, N, hop_div, frames, out, olen, int(threads))
     return out, used
 
 

@@ -64,23 +64,39 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 :
 // ------------------------------------------------------------------ K1 REF_COMPAT
 // kernel.cu:299-348: window (Hamming), zero-phase shift + zero pad to 2N, C2C 2N,
 // (|X|, atanf(Im/Re)) for all 2N bins.  The 2N-point transform of the real padded frame
-// is computed as an L = N point complex FFT + real split; bins > N by symmetry.
+// is an L = N point complex FFT + real split (bins 0 .. N); bins N+1 .. 2N-1 are the
+// conjugates of bins N-1 .. 1 (real input), i.e. the same magnitude and the negated phase.
+//
+// Geometry as K1 STANDARD: a wave walks a run of F frames, 4 runs per workgroup, no halo
+// (no unwrap).  Input: of the 2N padded samples only z[n] = (b[2n], b[2n+1]) with
+// n < N/4 (frame samples N/2 .. N-1) and n >= 3N/4 (frame samples 0 .. N/2-1) are nonzero,
+// so a lane's registers q < E/4 and q >= 3E/4 hold the frame's N samples (one contiguous
+// vector load of E/2 pairs, prefetched one frame ahead, kernel.cu:25-32's shift folded
+// into the register order) and the E/2 middle registers are compile-time zeros.
+// Output: every row store is a whole 512-byte block.  Block i < E holds bins 64 i + lane
+// (this lane's bins); mirror block j holds indices N + 64 j + lane = bins N - 64 j - lane,
+// which lane (64 - lane) & 63 holds in register E - j - 1 (lane 0: its own register E - j,
+// bin N itself for j = 0): a ds_bpermute lane reversal, as split_chunk_bp's partner read.
+// Phase: atanf(y/x) without the division (atan_ratio_pv2); magnitude: hardware sqrt.
 template <int L>
 __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
-    constexpr int N = L;  // window length
+    constexpr int N = L;          // window length
+    constexpr int QA = E / 4;     // registers 0 .. QA-1 and E-QA .. E-1 carry samples
+    constexpr int NST = 2 * E;    // row stores per frame (E blocks + E mirror blocks)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* twl = reinterpret_cast<float2*>(smem);
-    float2* twsl = twl + L;                            // L+1 split twiddles (+1 pad)
-    float2* tiles = twsl + (L + 2);
+    constexpr int TWN = ana_twl_n<L>();
+    float2* twl = reinterpret_cast<float2*>(smem);  // TWN stage-major twiddles
+    float2* twsl = twl + TWN;                        // L+1 split twiddles (+1 pad)
+    float2* tiles = twsl + (L + 2);                  // 4 x TILE
     float* winl = reinterpret_cast<float*>(tiles + 4 * G_::TILE);  // N window samples
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
-    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
+    for (int i = tid; i < TWN; i += 256) twl[i] = p.tw[i];
     for (int i = tid; i <= L; i += 256) twsl[i] = p.tws[i];
     for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
     __syncthreads();
@@ -91,39 +107,111 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
     float2* tile = tiles + w * G_::TILE;
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
+    const float2* w2 = reinterpret_cast<const float2*>(winl);
+    const int rev = ((64 - lane) & 63) << 2;
 
-    for (int u = 0; u < nfr; ++u) {
-        const int t = t0 + u;
-        const long long base = (long long)t * p.hop;
-        float2 z[E];
+    // frame samples 2 lane + 128 m + {0,1} (m < E/2) -> register q(m): m >= E/4 (samples
+    // N/2 ..) to q = m - E/4, m < E/4 (samples 0 .. N/2-1) to q = 3E/4 + m; x (window)
+    auto window = [&](const float2 (&xs)[E / 2], float2 (&z)[E]) {
 #pragma unroll
-        for (int q = 0; q < E; ++q) {
-            const int i = lane + 64 * q;
-            // b[2i], b[2i+1] of the shifted/padded 2N buffer (kernel.cu:25-32)
-            int src = -1;
-            if (2 * i < N / 2) src = 2 * i + N / 2;
-            else if (2 * i >= 3 * N / 2) src = 2 * i - 3 * N / 2;
-            float b0 = 0.0f, b1 = 0.0f;
-            if (src >= 0) {
-                const long long s = base + src;
-                const float x0 = (s < p.n) ? xc[s] : 0.0f;
-                const float x1 = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
-                b0 = x0 * winl[src];
-                b1 = x1 * winl[src + 1];
-            }
-            z[q] = make_float2(b0, b1);
+        for (int m = 0; m < E / 2; ++m) {
+            const int q = (m >= QA) ? m - QA : E - QA + m;
+            const float2 wv = lds_ld(&w2[lane + 64 * m]);
+            z[q] = make_float2(xs[m].x * wv.x, xs[m].y * wv.y);
         }
-        fft_run<L, false>(z, tile, twl, tw0, lane);
-        float2* srow = specc + (long long)t * p.spec_stride;
-        PV_FOR_BINS(E, lane, {
-            const float2 X = real_split<L>(tile, twsl, k);
-            const float mag = __builtin_sqrtf(X.x * X.x + X.y * X.y);
-            float ph = atanf(X.y / X.x);
-            if (X.x == 0.0f && X.y == 0.0f) ph = p.nan_faithful ? __builtin_nanf("") : 0.0f;
-            srow[k] = make_float2(mag, ph);
-            if (k != 0 && k != L) srow[2 * N - k] = make_float2(mag, -ph);
-        })
-        wave_lds_sync();
+#pragma unroll
+        for (int q = QA; q < E - QA; ++q) z[q] = make_float2(0.0f, 0.0f);
+    };
+    auto frame = [&](int u, float2 (&z)[E]) {
+        float2* srow = specc + (long long)(t0 + u) * p.spec_stride;
+        fft_run<L, false, false, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
+        float pm = 0.0f, pp = 0.0f;  // the previous bin's {mag, phase} (mirror source)
+        static_for<0, (E + 2) / 2>([&](auto ic) {
+            constexpr int i0 = 2 * decltype(ic)::value;
+            float2 X[2];
+            split_chunk_bp<L, 2, true, i0>(z, twsl, lane, X);  // 2X (TWICE): scale-free phase
+            const f2v ph2 = atan_ratio_pv2(X[0].y, X[0].x, X[1].y, X[1].x);
+            static_for<0, 2>([&](auto cc) {
+                constexpr int c2 = decltype(cc)::value;
+                constexpr int i = i0 + c2;
+                if constexpr (i <= E) {
+                    const float mag = 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    float ph = (c2 == 0) ? ph2.x : ph2.y;
+                    // atanf(0/0) = NaN of an all-zero bin (digital silence) when asked
+                    if (p.nan_faithful && X[c2].x == 0.0f && X[c2].y == 0.0f) ph = __builtin_nanf("");
+                    if constexpr (i < E)
+                        __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i + lane]));
+                    if constexpr (i >= 1) {
+                        // mirror block j = E - i: lane 0 sends bin 64 i (its register i), the
+                        // other lanes bin 64 (i - 1) + lane (register i - 1) to lane 64 - lane
+                        const float sm = (lane == 0) ? mag : pm;
+                        const float sp = (lane == 0) ? ph : pp;
+                        const float mm = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sm)));
+                        float mp = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sp)));
+                        if (!(i == E && lane == 0)) mp = -mp;  // conjugate; bin N is itself
+                        __builtin_nontemporal_store(f2v{mm, mp}, reinterpret_cast<f2v*>(&srow[N + 64 * (E - i) + lane]));
+                    }
+                    pm = mag;
+                    pp = ph;
+                }
+            });
+        });
+        wave_lds_sync();  // tile reads done before the next frame's pass_store
+    };
+    auto load_checked = [&](int u, float2 (&xs)[E / 2]) {
+        const long long base = (long long)(t0 + u) * p.hop;
+#pragma unroll
+        for (int m = 0; m < E / 2; ++m) {
+            const long long sidx = base + 2 * (lane + 64 * m);
+            xs[m].x = (sidx < p.n) ? xc[sidx] : 0.0f;
+            xs[m].y = (sidx + 1 < p.n) ? xc[sidx + 1] : 0.0f;
+        }
+    };
+    // frames whose N samples lie inside [0, n) (and 8-byte aligned) take vector loads
+    const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
+    const int ufast = (int)min((long long)nfr, max(0LL, lastfull - t0 + 1));
+    if constexpr (NST <= 63) {  // vmcnt holds 6 bits: the self-tracked prefetch (L <= 1024)
+        if (ufast > 0) {
+            float2 z[E];
+            {
+                f2v xv[E / 2];
+                gload_pairs<E / 2>(xv, xc + (long long)t0 * p.hop + 2 * lane);
+                vm_wait<0>(xv);
+                float2 xs[E / 2];
+#pragma unroll
+                for (int m = 0; m < E / 2; ++m) xs[m] = make_float2(xv[m].x, xv[m].y);
+                window(xs, z);
+            }
+            for (int u = 0; u < ufast; ++u) {
+                f2v xv[E / 2];  // frame u+1 (clamped), in flight during frame u
+                gload_pairs<E / 2>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
+                frame(u, z);  // exactly NST row stores
+                vm_wait<NST>(xv);
+                float2 xs[E / 2];
+#pragma unroll
+                for (int m = 0; m < E / 2; ++m) xs[m] = make_float2(xv[m].x, xv[m].y);
+                window(xs, z);
+            }
+        }
+    } else if (ufast > 0) {  // L = 2048: compiler-tracked prefetch
+        float2 xs[E / 2];
+        const float* src0 = xc + (long long)t0 * p.hop + 2 * lane;
+#pragma unroll
+        for (int m = 0; m < E / 2; ++m) xs[m] = *reinterpret_cast<const float2*>(src0 + 128 * m);
+        for (int u = 0; u < ufast; ++u) {
+            float2 z[E];
+            window(xs, z);
+            const float* src = xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane;
+#pragma unroll
+            for (int m = 0; m < E / 2; ++m) xs[m] = *reinterpret_cast<const float2*>(src + 128 * m);
+            frame(u, z);
+        }
+    }
+    for (int u = ufast; u < nfr; ++u) {
+        float2 xs[E / 2], z[E];
+        load_checked(u, xs);
+        window(xs, z);
+        frame(u, z);
     }
 }
 
@@ -135,7 +223,7 @@ static size_t ana_lds_std(bool ekl) {
 }
 template <int L>
 static size_t ana_lds_compat() {
-    return sizeof(float2) * (L + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * L;
+    return sizeof(float2) * (ana_twl_n<L>() + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * L;
 }
 // twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with register
 // overlap-add at L <= 512 the gains live in registers and gainl is not allocated

@@ -264,6 +264,52 @@ __device__ __forceinline__ f2v atan2_pv2(float y0, float x0, float y1, float x1)
     return f2v{__builtin_copysignf(r0, y0), __builtin_copysignf(r1, y1)};
 }
 
+// REF_COMPAT's atanf(y / x) (kernel.cu:101-109, range (-pi/2, pi/2]: the quadrant is lost)
+// without the division, for a pair of bins: atan2_pv2's reduction and polynomial without
+// its x < 0 fix-up, signed by sign(x) * sign(y) (y / x of signed zeros and infinities
+// included: 0 / -0 -> -0 ... and +-y / 0 -> +-pi/2 with the signs of the quotient).
+// Within 2.7e-7 rad of atanf; REF_COMPAT parity is tolerance based.  x = y = 0 gives +-0
+// (the caller substitutes the reference's NaN when asked).
+__device__ __forceinline__ f2v atan_ratio_pv2(float y0, float x0, float y1, float x1) {
+    f2v mx, mn, r;
+    float t0, t1, u0, u1;
+    asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(t0) : "v"(x0), "v"(y0), "s"(0x1p-126f));
+    asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(t1) : "v"(x1), "v"(y1), "s"(0x1p-126f));
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(u0) : "v"(x0), "v"(y0));
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(u1) : "v"(x1), "v"(y1));
+    mx = f2v{t0, t1};
+    mn = f2v{u0, u1};
+    r = f2v{__uint_as_float(0x7EF311C3u - __float_as_uint(t0)), __uint_as_float(0x7EF311C3u - __float_as_uint(t1))};
+    const f2v one = f2v{1.0f, 1.0f};
+    f2v e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    e = __builtin_elementwise_fma(-mx, r, one);
+    r = __builtin_elementwise_fma(r, e, r);
+    const f2v a = mn * r;
+    const f2v sq = a * a;
+    auto c = [](float v) { return f2v{v, v}; };
+    f2v p = c(-0x1.8ba68ap-10f);
+    p = __builtin_elementwise_fma(p, sq, c(0x1.398008p-7f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.d2ca58p-6f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.c2c9f4p-5f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.506f6cp-4f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.bd9028p-4f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.23c87ap-3f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.9986ecp-3f));
+    p = __builtin_elementwise_fma(p, sq, c(-0x1.5554eep-2f));
+    p = __builtin_elementwise_fma(p, sq, c(0x1.000000p+0f));
+    const f2v rr = a * p;
+    float r0 = rr.x, r1 = rr.y;
+    if (__builtin_fabsf(y0) > __builtin_fabsf(x0)) r0 = kHalfPi - r0;
+    if (__builtin_fabsf(y1) > __builtin_fabsf(x1)) r1 = kHalfPi - r1;
+    // sign of y / x: sign bit of y XOR sign bit of x
+    const unsigned s0 = (__float_as_uint(y0) ^ __float_as_uint(x0)) & 0x80000000u;
+    const unsigned s1 = (__float_as_uint(y1) ^ __float_as_uint(x1)) & 0x80000000u;
+    return f2v{__uint_as_float(__float_as_uint(r0) | s0), __uint_as_float(__float_as_uint(r1) | s1)};
+}
+
 // sin/cos of 2 pi rev: the hardware v_sin_f32 / v_cos_f32 (inputs in revolutions,
 // quarter-rate transcendental; they reduce their input themselves over [-256, 256]
 // revolutions, and every caller passes |rev| < 4: output phases are carried reduced;

@@ -65,3 +65,18 @@ def test_metric_matches_baseline_json():
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
     assert bench.METRIC == base["metric"]
     assert bench.HBM_PEAK_GBS == 8000.0
+
+
+def test_compat_oracle_batch_and_baseline():
+    """The REF_COMPAT workload's checker and CPU baseline: the OpenMP batch equals the
+    per-channel fp64 restatement."""
+    import pvref
+    x = bench.synth_channels_np(3, 20000, 20240)
+    out, used = pvref.compat_process_batch(x, 1024, 4, threads=2)
+    for c in range(3):
+        assert np.max(np.abs(out[c] - pvref.compat_process(x[c], 1024, 4))) <= 1e-6
+    frames = pvref.num_frames(20000, 256)
+    chk = bench.oracle_check(x, out[[0, 2]].copy(), [0, 2], 1024, 4, ord("t"), 1.0, frames, True, compat=True)
+    assert chk["pass"] and "compat" in chk["oracle"]
+    cpu = bench.cpu_baseline(x, 1024, 4, ord("t"), 1.0, target_s=0.2, compat=True)
+    assert cpu["value"] > 0 and "REF_COMPAT" in cpu["sample"]
