@@ -282,7 +282,6 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
             PV_FOR_BINS(E, lane, {
                 if (i < E || !packed) sv[i] = srow[k];
             })
-            unpack(sv);
         };
         if (nfr > 0) load_row(specc + (long long)t0 * p.spec_stride);
         for (int u = 0; u < p.F; ++u) {
@@ -291,6 +290,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
                 float2 cur[E + 1];
 #pragma unroll
                 for (int i = 0; i <= E; ++i) cur[i] = sv[i];
+                unpack(cur);  // at use: unpacking at the load would wait for it at once
                 if (u + 1 < nfr) load_row(specc + (long long)(t + 1) * p.spec_stride);
                 float2 z[E];
                 synth(u, t, cur, z);
