@@ -866,7 +866,6 @@ struct pv_rt {
     int direct = 0;  // PV_RT_LAUNCH=direct: launch pv_rt_push per callback instead of replaying
                      // the captured graph (BASELINE config 5's form, the default): measured p50
                      // 21 vs 28 us per callback on ROCm 7.2
-    int spin = 0;    // PV_RT_WAIT=spin: poll the stream instead of a blocking synchronise
 };
 
 namespace {
@@ -1006,9 +1005,6 @@ pv_status pv_rt_push(pv_rt* rt, const float* in, long long ldi, int nframes, flo
     return PV_OK;
 }
 
-#ifndef PV_RT_ZERO_COPY
-#define PV_RT_ZERO_COPY 1
-#endif
 pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     if (!rt) return fail(PV_ERR_ARG, "null rt");
     if (nframes <= 0) return fail(PV_ERR_ARG, "nframes must be > 0");
@@ -1021,14 +1017,13 @@ pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     // pinned, device-mapped host buffers: the captured kernel reads the callback's input
     // and writes its output in place over the bus (zero-copy: the graph is one kernel
     // node, no copy nodes); if the runtime cannot map them, the graph copies H2D / D2H
-    // around the kernel instead (PV_RT_ZERO_COPY=0 forces that form)
+    // around the kernel instead
     PV_HIP(hipHostMalloc((void**)&rt->h_in, sizeof(float) * C * ni, hipHostMallocMapped));
     PV_HIP(hipHostMalloc((void**)&rt->h_out, sizeof(float) * C * no, hipHostMallocMapped));
     std::memset(rt->h_in, 0, sizeof(float) * C * ni);
     std::memset(rt->h_out, 0, sizeof(float) * C * no);
     float *m_in = nullptr, *m_out = nullptr;
-    bool zero_copy = PV_RT_ZERO_COPY &&
-                     hipHostGetDevicePointer((void**)&m_in, rt->h_in, 0) == hipSuccess &&
+    bool zero_copy = hipHostGetDevicePointer((void**)&m_in, rt->h_in, 0) == hipSuccess &&
                      hipHostGetDevicePointer((void**)&m_out, rt->h_out, 0) == hipSuccess && m_in && m_out;
     if (!zero_copy) {
         (void)hipGetLastError();
@@ -1066,8 +1061,6 @@ pv_status pv_rt_capture(pv_rt* rt, int nframes) {
     rt->m_out = zero_copy ? m_out : nullptr;
     const char* lv = std::getenv("PV_RT_LAUNCH");
     rt->direct = (zero_copy && lv && std::string(lv) == "direct") ? 1 : 0;
-    const char* wv = std::getenv("PV_RT_WAIT");
-    rt->spin = (wv && std::string(wv) == "spin") ? 1 : 0;
     return PV_OK;
 }
 
@@ -1092,14 +1085,7 @@ pv_status pv_rt_callback(pv_rt* rt, const float* in, float* out) {
     } else {
         PV_HIP(hipGraphLaunch(rt->exec, rt->g_stream));
     }
-    if (rt->spin) {
-        hipError_t q;
-        while ((q = hipStreamQuery(rt->g_stream)) == hipErrorNotReady) {
-        }
-        if (q != hipSuccess) return fail(PV_ERR_HIP, std::string("pv_rt_callback: ") + hipGetErrorString(q));
-    } else {
-        PV_HIP(hipStreamSynchronize(rt->g_stream));
-    }
+    PV_HIP(hipStreamSynchronize(rt->g_stream));
     if (out && out != rt->h_out) std::memcpy(out, rt->h_out, sizeof(float) * C * no);
     return PV_OK;
 }

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Standalone driver for rocprofv3 counter passes: config 3 (1024 ch x 10 s, N=1024,
-hop=256, PV_STANDARD stretch 0.5) through pv_process, `--reps` times."""
+hop=256, PV_STANDARD stretch 0.5, packed rows as bench.py) through pv_process, `--reps`
+times; --N / --effect / --scale / --mode / --layout select the other workloads."""
 import argparse
 import os
 import sys
@@ -19,13 +20,16 @@ def main():
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--mode", default="standard")
     ap.add_argument("--calib", action="store_true")
+    ap.add_argument("--layout", choices=["packed", "natural"], default="packed")
     args = ap.parse_args()
     import torch
     from bench import synth_channels_np
     from pvamd import PhaseVocoder
+    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED
     n = 441000
+    layout = PV_SPEC_PACKED if (args.layout == "packed" and args.mode == "standard") else PV_SPEC_NATURAL
     pv = PhaseVocoder(args.N, args.effect, args.scale, 4, mode=args.mode,
-                      max_channels=args.channels, max_frames=2000)
+                      max_channels=args.channels, max_frames=2000, spec_layout=layout)
     # host-generated input + plain copy: no torch compute kernels in the profiled process
     x = torch.from_numpy(synth_channels_np(args.channels, n, 20240)).to("cuda:0")
     frames = pv.num_frames(n)
