@@ -32,6 +32,14 @@
  *
  * Errors: status codes instead of the reference's print-and-exit (io.cpp:115-124).  The
  * header-only C++ drop-in (include/phaseVocoder.h) restores print-and-exit on top.
+ *
+ * Environment overrides (read by pv_create / pv_rt_capture; the tests use them to reach
+ * every kernel geometry; none changes a result beyond run-boundary roundings):
+ *   PV_RUN_FRAMES=F      frames per wave run of the split path (even, 8..256)
+ *   PV_SYN_LANEK=0       per-bin unwrap constants from LDS instead of per-lane registers
+ *   PV_FUSED=0           the split path even where the q = 1 single launch applies
+ *   PV_FUSED_FRAMES=F    frames per run of the q = 1 single launch
+ *   PV_RT_LAUNCH=direct  pv_rt_callback launches the kernel instead of replaying the graph
  */
 #ifndef PV_H
 #define PV_H
