@@ -288,25 +288,57 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             // (ratios < 1) are summed in order like the oracle.  The ratio test is hoisted
             // out of the bin loop (wave-uniform): inside it the compiler merges it with the
             // per-lane count test into an exec-masked branch per bin (17 at L = 1024).
-#define PV_PITCH_GATHER(MULTI_)                                                   \
-            PV_FOR_BINS(E, lane, {                                                \
-                const i2v sc = lds_ld2i(&srcl[2 * k]);                            \
-                const int s = sc.x;                                               \
-                const float2 f = lds_ld(&tile[G_::pad(s >= 0 ? s : 0)]);          \
-                float ms = (s >= 0) ? f.x : 0.0f;                                 \
-                const float pc = (s >= 0) ? f.y : 0.0f;                           \
-                if (MULTI_)                                                       \
-                    for (int qq = 1; qq < sc.y; ++qq) ms += tile[G_::pad(s + qq)].x; \
-                float sn, cs;                                                     \
-                sincos_rev(pc, &sn, &cs);                                         \
-                Y[i] = make_float2(ms * cs, ms * sn);                             \
-            })
+            // The LDS reads are issued in groups of G bins (all map reads, then all tile
+            // reads, then the arithmetic): the volatile LDS loads keep program order, so bin
+            // by bin every map read -> tile read pair would be two serialized LDS round trips
+            // per bin (34 per frame at L = 1024).
+            // (config 4 synthesis -2.5 %; 1 at L <= 512, whose kernels sit at their VGPR budget)
+            constexpr int G = (L >= 1024) ? 4 : 1;
+            auto gather = [&](auto multi_tag) {
+                constexpr bool MULTI = decltype(multi_tag)::value;
+                static_for<0, (E + G) / G>([&](auto ig) {
+                    constexpr int i0 = decltype(ig)::value * G;
+                    i2v sc[G];
+                    float2 f[G];
+                    static_for<0, G>([&](auto jj) {
+                        constexpr int j = decltype(jj)::value;
+                        constexpr int i = i0 + j;
+                        if constexpr (i <= E) {
+                            const int k = (i == E) ? L : lane + 64 * i;
+                            if (i < E || lane == 0) sc[j] = lds_ld2i(&srcl[2 * k]);
+                        }
+                    });
+                    static_for<0, G>([&](auto jj) {
+                        constexpr int j = decltype(jj)::value;
+                        constexpr int i = i0 + j;
+                        if constexpr (i <= E) {
+                            const int sidx = sc[j].x;
+                            if (i < E || lane == 0) f[j] = lds_ld(&tile[G_::pad(sidx >= 0 ? sidx : 0)]);
+                        }
+                    });
+                    static_for<0, G>([&](auto jj) {
+                        constexpr int j = decltype(jj)::value;
+                        constexpr int i = i0 + j;
+                        if constexpr (i <= E) {
+                            if (i < E || lane == 0) {
+                                const int sidx = sc[j].x;
+                                float ms = (sidx >= 0) ? f[j].x : 0.0f;
+                                const float pc = (sidx >= 0) ? f[j].y : 0.0f;
+                                if constexpr (MULTI)
+                                    for (int qq = 1; qq < sc[j].y; ++qq) ms += tile[G_::pad(sidx + qq)].x;
+                                float sn, cs;
+                                sincos_rev(pc, &sn, &cs);
+                                Y[i] = make_float2(ms * cs, ms * sn);
+                            }
+                        }
+                    });
+                });
+            };
             if (pm.multi) {
-                PV_PITCH_GATHER(true)
+                gather(std::true_type{});
             } else {
-                PV_PITCH_GATHER(false)
+                gather(std::false_type{});
             }
-#undef PV_PITCH_GATHER
             wave_lds_sync();
             PV_FOR_BINS(E, lane, {
                 float2 y = Y[i];

@@ -44,8 +44,11 @@ struct FuGeo {
     static_assert(O_SRC % 2 == 0 && O_TILE % 4 == 0, "alignment of the LDS carve-up");
 };
 
+// 4 waves per SIMD (<= 128 VGPRs): a single stream's runs (config 2: 3445 waves) then fit the
+// chip in one round (at 131 VGPRs, 3 per SIMD, a tenth of them ran as a second round:
+// config 2 fused 53.5-55.2 -> 45.2-46.2 us)
 template <int L, int MODE, int DT>
-__global__ __launch_bounds__(256) void k_fused(FusedParams p) {
+__global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
     using G_ = Geo<L>;
     using FG = FuGeo<L>;
     constexpr int E = G_::E;
