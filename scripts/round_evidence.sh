@@ -13,13 +13,14 @@ run() {  # name seconds cmd...
   echo "$name rc=$rc"; grep '^{' gpurun_out/$name.log | tail -1 | cut -c1-400
   if [ $rc -ne 0 ]; then tail -20 gpurun_out/$name.log; exit $rc; fi
 }
-STEPS="${STEPS:-tests c3 c2 c4 rt prof pmc}"
+STEPS="${STEPS:-tests c3 c2 c4 compat rt prof pmc}"
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 700 python -m pytest tests -m gpu -q -rf; tail -3 gpurun_out/pytest_gpu.log ;;
+    tests) run pytest_gpu 700 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread; tail -3 gpurun_out/pytest_gpu.log ;;
     c3) run bench_c3 400 python bench.py ;;
     c2) run bench_c2 300 python bench.py --workload c2 ;;
     c4) run bench_c4 300 python bench.py --workload c4 --no-cpu ;;
+    compat) run bench_compat 300 python bench.py --workload compat ;;
     rt) run bench_rt 300 python bench.py --workload rt ;;
     prof)
       rm -rf gpurun_out/prof

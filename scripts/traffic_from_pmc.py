@@ -55,5 +55,6 @@ for k, cs in per.items():
                                            "write_bytes_per_launch": wr,
                                            "bytes_per_launch": rd + wr}
 res["_workload"] = os.environ.get("PV_TRAFFIC_WORKLOAD", "c3")  # what prof_kernels.py ran
+res["_layout"] = os.environ.get("PV_TRAFFIC_LAYOUT", "packed")   # its spectrum row layout
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
