@@ -85,11 +85,14 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         // the last pass's registers feed the split directly (no final image in LDS)
         fft_run<L, false, false, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
         [[maybe_unused]] float mag0 = 0.0f, ph0 = 0.0f;  // packed: bin `lane` until slot 0 goes out
-        // bins in chunks of CH (bounded live registers), all reads of a chunk batched
+        // bins in chunks of CH (bounded live registers), all reads of a chunk batched; both
+        // layouts take bins in the order 0, L, 1 .. E-1 (bin_at<E, true>): in natural order
+        // the L = 1024 natural-row kernels spill 1-2 VGPRs at 168 (3 waves/SIMD), which the
+        // self-tracked prefetch must never see (tests/test_abi.py)
         static_for<0, (E + CH) / CH>([&](auto ic) {
             constexpr int p0 = decltype(ic)::value * CH;
             float2 X[CH];
-            split_chunk_bp<L, CH, true, p0, PACKED>(z, twsl, lane, X);
+            split_chunk_bp<L, CH, true, p0, true>(z, twsl, lane, X);
             // phases of the chunk's bins: pairs through the packed atan2
             float phs[CH];
             static_for<0, CH / 2>([&](auto jj) {
@@ -106,7 +109,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             static_for<0, CH>([&](auto cc) {
                 constexpr int c2 = decltype(cc)::value;
                 if constexpr (p0 + c2 <= E) {
-                    constexpr int i = bin_at<E, PACKED>(p0 + c2);
+                    constexpr int i = bin_at<E, true>(p0 + c2);
                     const int k = (i == E) ? L : lane + 64 * i;
                     (void)k;
                     const float ph = phs[c2];

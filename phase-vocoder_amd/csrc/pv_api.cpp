@@ -117,6 +117,10 @@ struct pv_handle {
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
     int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
+#ifdef PV_FUSED_STAMPS
+    unsigned long long* d_stamps = nullptr;  // diagnostic build: per-wave phase stamps of k_fused
+    size_t n_stamps = 0;
+#endif
     Profile prof;
 };
 
@@ -355,6 +359,9 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     p.tail_len = h->tail_len;
     p.seam_flags = h->d_seam_flags;
     p.packed = h->packed;
+#ifdef PV_FUSED_STAMPS
+    p.stamps = h->d_stamps;
+#endif
     PV_LAUNCH(h, KF, s, pv::launch_fused(h->L_syn, h->pitch ? 2 : 0, C, p, s));
     return PV_OK;
 }
@@ -411,6 +418,20 @@ pv_status pv_get_info(const pv_handle* h, pv_info* info) {
     return PV_OK;
 }
 
+#ifdef PV_FUSED_STAMPS
+// diagnostic build only (make variant NAME=stamps DEFS=-DPV_FUSED_STAMPS): the per-wave
+// phase stamps of the last k_fused launch, kFusedStampSlots per wave (scripts/fused_stamps.py)
+pv_status pv_debug_stamps(const pv_handle* h, unsigned long long* dst, size_t count) {
+    if (!h || !dst || !h->d_stamps) return PV_ERR_ARG;
+    DeviceGuard g(h->cfg.device);
+    if (hipDeviceSynchronize() != hipSuccess) return PV_ERR_HIP;
+    if (hipMemcpy(dst, h->d_stamps, sizeof(unsigned long long) * std::min(count, h->n_stamps),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return PV_ERR_HIP;
+    return PV_OK;
+}
+#endif
+
 void pv_destroy(pv_handle* h) {
     if (!h) return;
     DeviceGuard g(h->cfg.device);
@@ -419,6 +440,9 @@ void pv_destroy(pv_handle* h) {
                     h->d_carry, h->d_tails, h->d_seam_flags};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+#ifdef PV_FUSED_STAMPS
+    if (h->d_stamps) (void)hipFree(h->d_stamps);
+#endif
     for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
     for (auto e : h->prof.ev_stop) (void)hipEventDestroy(e);
     for (auto e : h->prof.pool) (void)hipEventDestroy(e);
@@ -641,6 +665,11 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if (h->F_fused > 0) {
         PV_HIP(hipMalloc((void**)&h->d_seam_flags, sizeof(int) * wg_total));
         PV_HIP(hipMemset(h->d_seam_flags, 0, sizeof(int) * wg_total));
+#ifdef PV_FUSED_STAMPS
+        h->n_stamps = wg_total * 4 * pv::kFusedStampSlots;
+        PV_HIP(hipMalloc((void**)&h->d_stamps, sizeof(unsigned long long) * h->n_stamps));
+        PV_HIP(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * h->n_stamps));
+#endif
     }
 
     // LDS budget check for the synthesis kernel (largest)

@@ -66,22 +66,20 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
-    float2 tw0[E];
-    load_tw0<L>(tw0, p.tw);
-    for (int i = tid; i < L; i += 256) twl[i] = p.tw[i];
-    for (int i = tid; i < B; i += 256) {
-        twsl[i] = p.tws[i];
-        if (MODE == 2) { srcl[2 * i] = p.src_first[i]; srcl[2 * i + 1] = p.src_cnt[i]; }
-    }
-    for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
-    float2 gn[NS];  // synthesis gains of the lane's OLA slots (frame-invariant)
-    {
-        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) gn[s] = g2[64 * s + lane];
-    }
-    __syncthreads();
-
+#ifdef PV_FUSED_STAMPS
+    // diagnostic build (scripts/fused_stamps.py): s_memrealtime (100 MHz) at the phase
+    // boundaries of every wave, written by lane 0 with vector stores
+    unsigned long long* stp =
+        p.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * kFusedStampSlots;
+    const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long st_mt0 = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](int slot, unsigned long long v) {
+        if (lane == 0 && slot < kFusedStampSlots) stp[slot] = v;
+    };
+#define PV_STAMP(slot_) stamp((slot_), __builtin_amdgcn_s_memrealtime())
+#else
+#define PV_STAMP(slot_) ((void)0)
+#endif
     const int c = blockIdx.y;
     const int run = blockIdx.x * 4 + w;
     const int t0 = run * p.F;
@@ -124,8 +122,54 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
         }
     };
 
+    // frame t0's samples are requested before the table set-up, whose latency hides theirs
     float2 xr[E];
     if (nfr > 0) load(t0, xr);
+
+    // tables -> LDS: every load issued before the first LDS write, so the set-up costs one
+    // round trip instead of one per loop trip (config 2 stamps: 2.6 us of a 27.6 us wave)
+    float2 tw0[E];
+    float2 gn[NS];  // synthesis gains of the lane's OLA slots (frame-invariant)
+    {
+        constexpr int KT = (L + 255) / 256, KB = (B + 255) / 256, KW = N / 256;
+        static_assert(N % 256 == 0, "window in whole 256-thread trips");
+        float2 ttw[KT], tts[KB];
+        int tsf[KB], tsc[KB];
+        float twn[KW];
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+            if (tid + 256 * k < L) ttw[k] = p.tw[tid + 256 * k];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            const int i = tid + 256 * k;
+            if (i < B) {
+                tts[k] = p.tws[i];
+                if (MODE == 2) { tsf[k] = p.src_first[i]; tsc[k] = p.src_cnt[i]; }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KW; ++k) twn[k] = p.win[tid + 256 * k];
+        load_tw0<L>(tw0, p.tw);
+        const float2* g2 = reinterpret_cast<const float2*>(p.gain);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) gn[s] = g2[64 * s + lane];
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+            if (tid + 256 * k < L) twl[tid + 256 * k] = ttw[k];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            const int i = tid + 256 * k;
+            if (i < B) {
+                twsl[i] = tts[k];
+                if (MODE == 2) { srcl[2 * i] = tsf[k]; srcl[2 * i + 1] = tsc[k]; }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KW; ++k) winl[tid + 256 * k] = twn[k];
+    }
+    __syncthreads();
+    PV_STAMP(2);
+
     for (int u = 0; u < p.F; ++u) {
         const int t = t0 + u;
         if (u < nfr) {
@@ -139,6 +183,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                     z[q].y = xr[q].y * wv.y;
                 }
             }
+            if (u == 0) PV_STAMP(10);  // frame 0's samples have landed (F <= 7)
             if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
             // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv.  The
             // split reads the final image in LDS (the register split, split_chunk_bp, costs
@@ -147,24 +192,35 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
             fft_run<L, false, true>(z, tile, twl, tw0, lane);
             float2 sv[E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
-            constexpr int CH = 3;
+            // bins in pairs: the phases of a pair through the packed-fp32 atan2 (atan2_pv2,
+            // bit-identical to atan2_pv per half)
+            constexpr int CH = 2;
             static_for<0, (E + CH) / CH>([&](auto ic) {
                 constexpr int i0 = decltype(ic)::value * CH;
                 float2 X[CH];
                 split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
-#pragma unroll
-                for (int c2 = 0; c2 < CH; ++c2) {
-                    const int i = i0 + c2;
-                    if (i > E) break;
-                    const float ph = atan2_pv(X[c2].y, X[c2].x);
-                    float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
-                    mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
-                    sv[i] = make_float2(mag, ph);
-                    // bin L (i = E): the same value and address on every lane (natural layout
-                    // only; packed rows carry it in slot 0); bins 0..63 go out below
-                    if (i > 0 && (i < E || !p.packed))
-                        __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+                float phs[CH];
+                if constexpr (i0 + 1 <= E) {
+                    const f2v ph2 = atan2_pv2(X[0].y, X[0].x, X[1].y, X[1].x);
+                    phs[0] = ph2.x;
+                    phs[1] = ph2.y;
+                } else {
+                    phs[0] = atan2_pv(X[0].y, X[0].x);
                 }
+                static_for<0, CH>([&](auto cc) {
+                    constexpr int c2 = decltype(cc)::value;
+                    constexpr int i = i0 + c2;
+                    if constexpr (i <= E) {
+                        const float ph = phs[c2];
+                        float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                        mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
+                        sv[i] = make_float2(mag, ph);
+                        // bin L (i = E): the same value and address on every lane (natural
+                        // layout only; packed rows carry it in slot 0); bins 0..63 go out below
+                        if (i > 0 && (i < E || !p.packed))
+                            __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+                    }
+                });
             });
             {
                 // slot 0: PV_SPEC_PACKED lane 0 carries bins 0 and L (both real)
@@ -206,9 +262,28 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) acc[s] = (s + D < NS) ? acc[(s + D < NS) ? s + D : 0] : make_float2(0.0f, 0.0f);
+        if (u < 6) PV_STAMP(3 + u);
     }
+    PV_STAMP(11);  // frames end; slots 3..9 = frames 0..6
+#ifdef PV_FUSED_STAMPS
+    __syncthreads();
+    PV_STAMP(9);  // the workgroup's slowest wave has finished its frames (F <= 6)
+#endif
     close_seams_inline<L, NS, D>(acc, tiles, w, lane, c, blockIdx.x, (p.nruns + 3) / 4, obase, p.F, hs, outc,
-                                 p.out_len, p.tails, p.tail_len, p.seam_flags);
+                                 p.out_len, p.out_aligned != 0, p.tails, p.tail_len, p.seam_flags);
+#ifdef PV_FUSED_STAMPS
+    {
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
+        stamp(0, st_rt0);
+        stamp(1, st_mt0);
+        stamp(12, rt1);
+        stamp(13, mt1);
+        // HW_ID (CU / SIMD / SE) and XCC_ID
+        stamp(14, (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)));
+        stamp(15, (unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)));
+    }
+#endif
+#undef PV_STAMP
 }
 
 bool fused_supported(int L, int hs) {
@@ -216,28 +291,40 @@ bool fused_supported(int L, int hs) {
            hs <= L;
 }
 
+// only the geometries fused_supported admits are instantiated (out hop <= L)
+template <int LL, int MM, int DT>
+static hipError_t launch_fused_t(dim3 grid, const FusedParams& p, hipStream_t s) {
+    if constexpr (128 * DT <= LL) {
+        hipLaunchKernelGGL((k_fused<LL, MM, DT>), grid, dim3(256), FuGeo<LL>::BYTES, s, p);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
+template <int LL, int MM>
+static hipError_t launch_fused_l(int dt, dim3 grid, const FusedParams& p, hipStream_t s) {
+    switch (dt) {
+        case 1: return launch_fused_t<LL, MM, 1>(grid, p, s);
+        case 2: return launch_fused_t<LL, MM, 2>(grid, p, s);
+        case 4: return launch_fused_t<LL, MM, 4>(grid, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+template <int MM>
+static hipError_t launch_fused_m(int L, int dt, dim3 grid, const FusedParams& p, hipStream_t s) {
+    switch (L) {
+        case 128: return launch_fused_l<128, MM>(dt, grid, p, s);
+        case 256: return launch_fused_l<256, MM>(dt, grid, p, s);
+        case 512: return launch_fused_l<512, MM>(dt, grid, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 // mode: 0 STANDARD stretch, 2 STANDARD pitch (q = 1 only; the caller checks)
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s) {
-    dim3 grid((p.nruns + 3) / 4, channels);
+    const dim3 grid((p.nruns + 3) / 4, channels);
     const int dt = p.hs / 128;
-#define PV_FU(LL_, MM_)                                                                                 \
-    switch (dt) {                                                                                       \
-        case 1: hipLaunchKernelGGL((k_fused<LL_, MM_, 1>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
-        case 2: hipLaunchKernelGGL((k_fused<LL_, MM_, 2>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
-        case 4: hipLaunchKernelGGL((k_fused<LL_, MM_, 4>), grid, dim3(256), FuGeo<LL_>::BYTES, s, p); break; \
-        default: return hipErrorInvalidValue;                                                           \
-    }
-#define PV_FU_L(MM_)                          \
-    switch (L) {                              \
-        case 128: PV_FU(128, MM_); break;     \
-        case 256: PV_FU(256, MM_); break;     \
-        case 512: PV_FU(512, MM_); break;     \
-        default: return hipErrorInvalidValue; \
-    }
-    if (mode == 2) { PV_FU_L(2); } else { PV_FU_L(0); }
-#undef PV_FU_L
-#undef PV_FU
-    return hipGetLastError();
+    return mode == 2 ? launch_fused_m<2>(L, dt, grid, p, s) : launch_fused_m<0>(L, dt, grid, p, s);
 }
 
 }  // namespace pv

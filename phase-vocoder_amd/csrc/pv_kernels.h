@@ -86,7 +86,13 @@ struct FusedParams {
     int tail_len;
     int* seam_flags;                   // [C][nwg] arrival counters, 0 between launches
     int packed;                        // PV_SPEC_PACKED rows
+#ifdef PV_FUSED_STAMPS
+    unsigned long long* stamps;        // diagnostic build only: kFusedStampSlots per wave
+#endif
 };
+#ifdef PV_FUSED_STAMPS
+constexpr int kFusedStampSlots = 16;  // rt start, mt start, setup, frame 0..F-1, loop, end rt/mt, hw id
+#endif
 
 struct SeamParams {
     float* out;

@@ -36,6 +36,23 @@ __device__ __forceinline__ int arrive(int* flag, int lane) {
     return __shfl(old, 0);
 }
 
+// K write-through 8-byte loads of a lane's positions base + 128 m (m < K), all in flight at
+// once; the caller's sc1_wait makes them (and everything else outstanding) land
+template <int K>
+__device__ __forceinline__ void ld_sc1_issue(f2v (&v)[K], const float* base) {
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        const float* pm = base + 1024 * (m >> 3);  // 13-bit signed immediate offsets
+        asm volatile("global_load_dwordx2 %0, %1, off offset:%2 sc1" : "=v"(v[m]) : "v"(pm), "n"(512 * (m & 7)) : "memory");
+    }
+}
+template <int K>
+__device__ __forceinline__ void sc1_wait(f2v (&v)[K]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < K; ++m) asm volatile("" : "+v"(v[m]));  // uses stay after the wait
+}
+
 // After a register overlap-add run (wave w of a workgroup of 4 consecutive runs, workgroup
 // index wg of nwg along the channel): the run's tail -> ring (LDS, over the tiles), the three
 // intra-workgroup seams from the neighbours' tails, and the inter-workgroup seams in the
@@ -46,12 +63,21 @@ __device__ __forceinline__ int arrive(int* flag, int lane) {
 // 1 reads the other part (sc1 loads), writes head + tail and resets the counter for the next
 // launch.  Nobody waits for anybody, so there is no dispatch-order assumption; head + tail
 // is the same float whoever adds it.  Every wave of the workgroup must call this.
+//
+// The overlap (TL = N - out hop) is TM = TL / 128 float2 per lane at positions 2 lane + 128 m:
+// every read-back of a seam is issued as one batch and waited for once (per element, a load
+// and its wait were 12 serialized round trips; config 2 stamps, scripts/fused_stamps.py: the
+// seams were 5.8 us of a 27.6 us wave, 11.3 us on wave 3).  Unaligned `out` takes the
+// per-sample path.
 template <int L, int NS, int D>
 __device__ __forceinline__ void close_seams_inline(const float2 (&acc)[NS], float2* tiles, int w, int lane, int c,
                                                    int wg, int nwg, long long obase, int F, int hs, float* outc,
-                                                   long long out_len, float* tails, int tail_len, int* seam_flags) {
+                                                   long long out_len, bool out_aligned, float* tails, int tail_len,
+                                                   int* seam_flags) {
     constexpr int N = 2 * L;
-    const int TL = N - hs;
+    constexpr int TL = N - 128 * D;  // = N - hs
+    constexpr int TM = TL / 128;
+    static_assert(TL % 128 == 0 && TM >= 1 && TM <= 16, "overlap in whole 128-sample blocks");
     __syncthreads();
     float* rings = reinterpret_cast<float*>(tiles);
     float* ring = rings + w * N;
@@ -61,46 +87,124 @@ __device__ __forceinline__ void close_seams_inline(const float2 (&acc)[NS], floa
         for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
     }
     __syncthreads();
-    // seams: run w's tail overlaps run w+1's head
-    if (w > 0) {
-        const float* prev = rings + (w - 1) * N;
-        for (int j = lane; j < TL; j += 64) {
-            const long long gp = obase + j;
-            if (gp < out_len) outc[gp] += prev[j];
-        }
-    }
-    if (w == 3) {
-        const bool last = (wg + 1 >= nwg);
-        float* tdst = tails + ((long long)c * nwg + wg) * tail_len;
-        const long long nbase = obase + (long long)F * hs;  // workgroup wg+1's first position
-        for (int j = lane; j < TL; j += 64) {
-            const float v = ring[j];
-            if (last) {
-                const long long gp = nbase + j;
-                if (gp < out_len) outc[gp] = v;
-            } else {
-                st_sc1(tdst + j, v);
+    const bool last = (wg + 1 >= nwg);
+    const long long nbase = obase + (long long)F * hs;  // workgroup wg+1's first position
+    if (!out_aligned) {
+        // seams: run w's tail overlaps run w+1's head
+        if (w > 0) {
+            const float* prev = rings + (w - 1) * N;
+            for (int j = lane; j < TL; j += 64) {
+                const long long gp = obase + j;
+                if (gp < out_len) outc[gp] += prev[j];
             }
         }
-        if (!last) {
-            int* flag = seam_flags + (long long)c * nwg + wg;
-            if (arrive(flag, lane) == 1) {  // workgroup wg+1's head is in out
-                for (int j = lane; j < TL; j += 64) {
+        if (w == 3) {
+            float* tdst = tails + ((long long)c * nwg + wg) * tail_len;
+            for (int j = lane; j < TL; j += 64) {
+                const float v = ring[j];
+                if (last) {
                     const long long gp = nbase + j;
-                    if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ring[j];
+                    if (gp < out_len) outc[gp] = v;
+                } else {
+                    st_sc1(tdst + j, v);
+                }
+            }
+            if (!last) {
+                int* flag = seam_flags + (long long)c * nwg + wg;
+                if (arrive(flag, lane) == 1) {  // workgroup wg+1's head is in out
+                    for (int j = lane; j < TL; j += 64) {
+                        const long long gp = nbase + j;
+                        if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ring[j];
+                    }
+                    if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        if (w == 0 && wg > 0) {
+            int* flag = seam_flags + (long long)c * nwg + (wg - 1);
+            if (arrive(flag, lane) == 1) {  // workgroup wg-1's tail is in tails
+                const float* tsrc = tails + ((long long)c * nwg + (wg - 1)) * tail_len;
+                for (int j = lane; j < TL; j += 64) {
+                    const long long gp = obase + j;
+                    if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ld_sc1(tsrc + j);
                 }
                 if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        return;
     }
+    // 8-byte path: positions are even and out_len is even (frames * hs + N - hs), so a pair
+    // is either wholly inside out or wholly past it
+    const float2* own2 = reinterpret_cast<const float2*>(ring) + lane;
+    // (1) w > 0: this run's head (stored in the frame loop) back, all loads in flight
+    f2v head[TM];
+    if (w > 0) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+            const long long gp = obase + 2 * lane + 128 * m;
+            head[m] = (gp < out_len) ? *reinterpret_cast<const f2v*>(outc + gp) : f2v{0.0f, 0.0f};
+        }
+    }
+    // (2) w = 3: the workgroup's last tail — final samples if this is the channel's last
+    // workgroup, else published write-through for seam wg + 1, then arrive
+    bool second = false;
+    if (w == 3) {
+        if (last) {
+#pragma unroll
+            for (int m = 0; m < TM; ++m) {
+                const long long gp = nbase + 2 * lane + 128 * m;
+                const float2 v = own2[64 * m];
+                if (gp < out_len) __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(outc + gp));
+            }
+        } else {
+            float* tdst = tails + ((long long)c * nwg + wg) * tail_len + 2 * lane;
+#pragma unroll
+            for (int m = 0; m < TM; ++m) {
+                const float2 v = own2[64 * m];
+                st_sc1(tdst + 128 * m, f2v{v.x, v.y});
+            }
+            second = arrive(seam_flags + (long long)c * nwg + wg, lane) == 1;
+        }
+    }
+    // (3) intra-workgroup seam: head + run w-1's tail
+    if (w > 0) {
+        const float2* prev2 = reinterpret_cast<const float2*>(rings + (w - 1) * N) + lane;
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+            const long long gp = obase + 2 * lane + 128 * m;
+            const float2 t = prev2[64 * m];
+            if (gp < out_len)
+                __builtin_nontemporal_store(f2v{head[m].x + t.x, head[m].y + t.y}, reinterpret_cast<f2v*>(outc + gp));
+        }
+    }
+    // (4) w = 3, second at seam wg + 1: workgroup wg+1's head is in out (inside out: that
+    // workgroup has frames)
+    if (second) {
+        f2v hd[TM];
+        ld_sc1_issue<TM>(hd, outc + nbase + 2 * lane);
+        sc1_wait<TM>(hd);
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+            const float2 v = own2[64 * m];
+            __builtin_nontemporal_store(f2v{hd[m].x + v.x, hd[m].y + v.y},
+                                        reinterpret_cast<f2v*>(outc + nbase + 2 * lane + 128 * m));
+        }
+        if (lane == 0) __hip_atomic_store(seam_flags + (long long)c * nwg + wg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // (5) w = 0 of workgroup wg > 0: arrive at seam wg; second: its head (inside out: wave 0
+    // has frames) + workgroup wg-1's tail
     if (w == 0 && wg > 0) {
         int* flag = seam_flags + (long long)c * nwg + (wg - 1);
-        if (arrive(flag, lane) == 1) {  // workgroup wg-1's tail is in tails
-            const float* tsrc = tails + ((long long)c * nwg + (wg - 1)) * tail_len;
-            for (int j = lane; j < TL; j += 64) {
-                const long long gp = obase + j;
-                if (gp < out_len) outc[gp] = ld_sc1(outc + gp) + ld_sc1(tsrc + j);
-            }
+        if (arrive(flag, lane) == 1) {
+            f2v hd[TM], tl[TM];
+            ld_sc1_issue<TM>(hd, outc + obase + 2 * lane);
+            ld_sc1_issue<TM>(tl, tails + ((long long)c * nwg + (wg - 1)) * tail_len + 2 * lane);
+            sc1_wait<TM>(hd);
+            sc1_wait<TM>(tl);
+#pragma unroll
+            for (int m = 0; m < TM; ++m)
+                __builtin_nontemporal_store(f2v{hd[m].x + tl[m].x, hd[m].y + tl[m].y},
+                                            reinterpret_cast<f2v*>(outc + obase + 2 * lane + 128 * m));
             if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }

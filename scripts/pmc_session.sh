@@ -9,7 +9,7 @@ i=0
 while IFS= read -r set; do
   [ -z "$set" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-include-regex "pv::" --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 scripts/prof_kernels.py ${PROF_ARGS:-} > gpurun_out/pmc/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --kernel-include-regex "pv::" --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 scripts/prof_kernels.py ${PROF_ARGS:-} > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($set) rc=$rc"
   case $rc in 124|134|137|139) echo FATAL; exit $rc;; esac
 done < "${PMC_SETS:-scripts/pmc_sets.txt}"

@@ -21,15 +21,16 @@ def main():
     ap.add_argument("--mode", default="standard")
     ap.add_argument("--calib", action="store_true")
     ap.add_argument("--layout", choices=["packed", "natural"], default="packed")
+    ap.add_argument("--n", type=int, default=441000, help="samples per channel (c2: 2646000)")
     args = ap.parse_args()
     import torch
     from bench import synth_channels_np
     from pvamd import PhaseVocoder
     from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED
-    n = 441000
+    n = args.n
     layout = PV_SPEC_PACKED if (args.layout == "packed" and args.mode == "standard") else PV_SPEC_NATURAL
     pv = PhaseVocoder(args.N, args.effect, args.scale, 4, mode=args.mode,
-                      max_channels=args.channels, max_frames=2000, spec_layout=layout)
+                      max_channels=args.channels, max_frames=n // (args.N // 4) + 2, spec_layout=layout)
     # host-generated input + plain copy: no torch compute kernels in the profiled process
     x = torch.from_numpy(synth_channels_np(args.channels, n, 20240)).to("cuda:0")
     frames = pv.num_frames(n)
