@@ -159,6 +159,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 20 for c2)")
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--prof-every", type=int, default=None,
+                    help="per-kernel hipEvents on every k-th timed step (default: every step; a "
+                         "single-launch step is timed as one block instead)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the timed CPU baseline")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the timed batch (profiling passes only)")
@@ -260,17 +263,31 @@ def main():
         pv.process(x, spec=spec, out=out)
     torch.cuda.synchronize(dev)
 
-    pv.profile(True)
+    # kernel durations for the roofline, on the launch stream (pv launches on torch's current
+    # stream).  A single-launch step (the q = 1 fused path, config 2) is timed as a block:
+    # one event pair around the timed loop / steps (back-to-back launches, no gaps: the
+    # rocprofv3 trace shows 0 us between them).  Otherwise libpv records an event pair around
+    # every launch; each event record costs the queue ~5.6 us, nothing at ms-scale kernels
+    # but 15 % of a 37-us one.  --prof-every k samples every k-th step instead.
+    block = bool(pv.single_launch) and not args.prof_every
+    prof_every = 0 if block else (args.prof_every or 1)
+    pv.profile(prof_every)
     pv.profile_reset()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(args.steps):
         pv.process(x, spec=spec, out=out)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
-    prof = pv.profile_read()
+    if block:
+        prof = {"fused": (ev0.elapsed_time(ev1), args.steps)}
+    else:
+        prof = pv.profile_read()
     pv.profile(False)
 
     dt_t = torch.tensor([dt], dtype=torch.float64, device=cdev)
@@ -372,6 +389,8 @@ def main():
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
             "measured_ceiling": ceiling,
             "kernels": kernels,
+            "kernel_timing": "block: one event pair around the timed loop" if block
+                             else f"per-launch event pairs, every {prof_every}-th step",
             "tables_broadcast": tables,
             "rms_vs_oracle": check,
             "cpu_baseline": cpu,

@@ -260,7 +260,9 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
 pv_status pv_test_overlap_add(const float* in, const float* win, const float* back, float* out,
                               int n, int hop, void* stream);
 
-/* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py). */
+/* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py).  enable:
+ * 0 off, 1 every launch, k > 1 the launches of every k-th pv_analysis / pv_resynthesis /
+ * pv_process call (an event record costs the queue a few us). */
 pv_status pv_profile_enable(pv_handle* h, int enable);
 /* names[i] (static strings), total ms and launch count of each kernel since the last
  * reset; returns number of kernels written (<= cap). Synchronises the recorded events. */

@@ -250,8 +250,10 @@ class PhaseVocoder:
                    "pv_import_tables")
 
     # -------------------------------------------------------------- profiling (bench.py)
-    def profile(self, enable: bool = True):
-        self._call(self._L.pv_profile_enable(self._h, 1 if enable else 0), "pv_profile_enable")
+    def profile(self, enable=True):
+        """enable: False/0 off, True/1 every launch, k > 1 every k-th call's launches."""
+        k = int(enable) if not isinstance(enable, bool) else (1 if enable else 0)
+        self._call(self._L.pv_profile_enable(self._h, k), "pv_profile_enable")
 
     def profile_read(self) -> dict:
         cap = 8
