@@ -13,18 +13,16 @@ namespace pv {
 // registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
 // EKL: the expected advance e_k from an LDS table; otherwise (64 a multiple of the hop
 // divisor, so e_k depends on k mod 64 only) one register per lane, e_k = ek[lane].
-#ifndef PV_ANA_WAVES512
-#define PV_ANA_WAVES512 4
-#endif
-#ifndef PV_ANA_WAVES1024
-#define PV_ANA_WAVES1024 3  // 154 VGPRs; LDS (with PV_ANA_TWSHARE) allows 3 workgroups per CU
-#endif
+// waves per SIMD the analysis is compiled for (__launch_bounds__): L = 512 at <= 128 VGPRs
+// (94 used), L = 1024 at <= 168 (LDS with the twiddle sharing allows 3 workgroups per CU)
+constexpr int kAnaWaves512 = 4;
+constexpr int kAnaWaves1024 = 3;
 // D > 0: hop = 128 D samples, so frame u+1's register q is frame u's register q + D and a
 // frame costs only its D new sample pairs per lane (the other E - D are shifted in
 // registers): 1/E of the frame's bytes leave L2 instead of all of them.
 // PACKED: the pv.h PV_SPEC_PACKED row layout (bin L folded into slot 0).
 template <int L, bool EKL, int D, bool PACKED>
-__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? PV_ANA_WAVES512 : (L == 1024) ? PV_ANA_WAVES1024 : 1) void k_std_analysis(AnaParams p) {
+__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;

@@ -29,12 +29,6 @@ namespace pv {
 // forms"): an agent-scope release/acquire pair would write back / invalidate whole caches
 // (buffer_wbl2 / buffer_inv) per workgroup.
 
-#ifdef PV_FUSED_NOSPEC
-constexpr bool kFusedNoSpec = true;  // timing-only diagnostic build: no spectrum row stores
-#else
-constexpr bool kFusedNoSpec = false;
-#endif
-
 template <int L>
 struct FuGeo {
     static constexpr int N = 2 * L;
@@ -223,7 +217,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                         sv[i] = make_float2(mag, ph);
                         // bin L (i = E): the same value and address on every lane (natural
                         // layout only; packed rows carry it in slot 0); bins 0..63 go out below
-                        if (i > 0 && (i < E || !p.packed) && !kFusedNoSpec)
+                        if (i > 0 && (i < E || !p.packed))
                             __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
                     }
                 });
@@ -233,7 +227,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                 const bool pk0 = p.packed && lane == 0;
                 const f2v s0 = pk0 ? f2v{pack_real_bin(sv[0].x, sv[0].y), pack_real_bin(sv[E].x, sv[E].y)}
                                    : f2v{sv[0].x, sv[0].y};
-                if (!kFusedNoSpec) __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+                __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
             }
             wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers

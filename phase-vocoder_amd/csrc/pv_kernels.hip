@@ -127,14 +127,14 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 //   DT = 0 (any out hop): per-wave LDS ring of N samples.
 // After the loop the three intra-workgroup seams are closed from the neighbours' tails in
 // LDS (one barrier); the workgroup's last tail goes to `tails` for k_seam.
-#ifndef PV_SYN_WAVES512
-#define PV_SYN_WAVES512 3  // waves per SIMD the L = 512 synthesis is compiled for
-#endif
-#ifndef PV_SYN_WAVES1024
-#define PV_SYN_WAVES1024 1  // waves per SIMD the L = 1024 synthesis is compiled for
-#endif
+// waves per SIMD the synthesis is compiled for (__launch_bounds__): L = 512 at <= 168
+// VGPRs; L = 1024 bounded at 1 only so that the compiler may use up to 256 VGPRs: the
+// kernels compile to <= 256 without AGPRs, so the 2 waves/SIMD their LDS sets hold
+// (tests/test_abi.py checks both)
+constexpr int kSynWaves512 = 3;
+constexpr int kSynWaves1024 = 1;
 template <int L, int MODE, int DT, bool QPOW2 = false, bool LANEK = false>
-__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? PV_SYN_WAVES512 : (L == 1024) ? PV_SYN_WAVES1024 : 1) void k_synthesis(SynParams p) {
+__global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (L == 1024) ? kSynWaves1024 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
     constexpr int E = G_::E;
