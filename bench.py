@@ -204,7 +204,11 @@ def main():
     # PV_DIST_BACKEND=gloo) share the devices round-robin
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     backend = os.environ.get("PV_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on ROCm
-    if world > 1:
+    # under torchrun (or launch_ranks) the process group is always formed, a single rank
+    # included: the N = 1 torchrun run exercises the same RCCL init, table broadcast and
+    # reductions as N = 8 (tests/test_gpu_bench_dist.py)
+    distributed = world > 1 or ("MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ)
+    if distributed:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -242,7 +246,7 @@ def main():
                       max_frames=pv_frames(n, N // hop_div), device=local, spec_layout=layout)
     frames = pv.num_frames(n)
     tables = None
-    if world > 1:  # init-time RCCL broadcast of rank 0's tables (north_star); not timed
+    if distributed:  # init-time RCCL broadcast of rank 0's tables (north_star); not timed
         from pvamd.dist import broadcast_tables
         same = broadcast_tables(pv, src=0)
         tables = {"bytes": int(pv.export_tables().numel()), "bit_identical_to_local": same}
@@ -256,7 +260,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -292,7 +296,7 @@ def main():
     pv.profile(False)
 
     dt_t = torch.tensor([dt], dtype=torch.float64, device=cdev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     total_frames = C * frames * world * args.steps
@@ -355,7 +359,7 @@ def main():
         finite = bool(torch.isfinite(out).all().item())
         check = oracle_check(x_host, out[idx].cpu().numpy(), idx, N, hop_div, ord(effect), scale,
                              frames, finite, compat=compat)
-        if world > 1:  # worst rank
+        if distributed:  # worst rank
             t = torch.tensor([check["max"], check["mean"], 0.0 if check["pass"] else 1.0,
                               0.0 if finite else 1.0], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -383,7 +387,7 @@ def main():
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
                        "out_hop": hop_s, "spec_layout": args.layout,
                        "parallelism": f"channel-shard x{world}",
-                       "dist_backend": backend if world > 1 else None},
+                       "dist_backend": backend if distributed else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
@@ -398,7 +402,7 @@ def main():
             "host_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -38,3 +38,30 @@ def test_bench_rejects_gpus_world_size_mismatch():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
                        env=env, capture_output=True, text=True, timeout=60)
     assert p.returncode != 0 and "WORLD_SIZE=3" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_under_torchrun_one_rank_rccl(cuda):
+    """The launch form of the driver's N-GPU runs (torch.distributed.run, one rank per GPU)
+    with the production backend: nccl = RCCL.  One rank is what one GPU allows; it forms
+    the RCCL group, broadcasts the tables and max-reduces the timing and the check exactly
+    as every rank of the 8-GPU run does."""
+    import socket
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "PV_DIST_BACKEND"):
+        env.pop(k, None)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "1", "--channels", "8", "--seconds", "1",
+                        "--steps", "3", "--warmup", "1", "--no-cpu"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["dist_backend"] == "nccl"
+    assert d["tables_broadcast"]["bit_identical_to_local"] is True
+    assert d["rms_vs_oracle"]["pass"] and d["rms_vs_oracle"]["ranks"] == 1
