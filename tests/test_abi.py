@@ -145,3 +145,17 @@ def test_create_rejects_bad_spec_layouts():
 def test_static_inline_helpers_are_not_abi_symbols():
     assert "pv_unpack_bins" not in _lib.declared_symbols()
     assert "pv_process" in _lib.declared_symbols()
+
+
+def test_fused_stamps_diagnostic_compiles():
+    """The one diagnostic build configuration left in the sources (PV_FUSED_STAMPS: per-wave
+    phase stamps of the config-2 single launch, scripts/fused_stamps.py) still compiles."""
+    import subprocess
+    csrc = os.path.join(_lib.ROOT, "phase-vocoder_amd", "csrc")
+    for src in ("pv_fused.hip", "pv_api.cpp"):
+        cmd = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+               "-DPV_FUSED_STAMPS", "-fPIC", "-c", os.path.join(csrc, src), "-o", os.devnull]
+        if src.endswith(".cpp"):
+            cmd[1:1] = ["-x", "hip"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
