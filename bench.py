@@ -370,7 +370,9 @@ def main():
     path_bytes = (4 * hop_a + 4 * hop_s + 8 * B + 8 * B_read) * C * frames * world * args.steps
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    # the CPU baseline is a rank-0, N = 1 figure (the contract's cpu_baseline): an N-rank run
+    # reports null rather than time the host while the other ranks wait
+    if rank == 0 and world == 1 and not args.no_cpu:
         try:
             cpu = cpu_baseline(x_host, N, hop_div, ord(effect), scale, single=(C == 1), compat=compat)
         except Exception as e:  # reported, never fatal for the GPU number
