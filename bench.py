@@ -160,7 +160,7 @@ def main():
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--prof-every", type=int, default=None,
-                    help="per-kernel hipEvents on every k-th timed step (default 2; a "
+                    help="per-kernel hipEvents on every k-th timed step (default 1; a "
                          "single-launch step is timed as one block instead)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the timed CPU baseline")
     ap.add_argument("--no-check", action="store_true",
@@ -272,10 +272,11 @@ def main():
     # one event pair around the timed loop / steps (back-to-back launches, no gaps: the
     # rocprofv3 trace shows 0 us between them).  Otherwise libpv records an event pair around
     # every launch; each event record costs the queue ~5.6 us, nothing at ms-scale kernels
-    # but 15 % of a 37-us one, and ~1 % of a 4-ms four-launch step: by default every second
-    # step carries them (--prof-every k: every k-th).
+    # but 15 % of a 37-us one (and ~1 % of a 4-ms four-launch step, which keeps them on every
+    # step so that every launch of the timed region is accounted for; --prof-every k samples
+    # every k-th step instead).
     block = bool(pv.single_launch) and not args.prof_every
-    prof_every = 0 if block else (args.prof_every or 2)
+    prof_every = 0 if block else (args.prof_every or 1)
     pv.profile(prof_every)
     pv.profile_reset()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
