@@ -10,8 +10,9 @@
 // frame, no run records and no second pass over the spectrum.  The spectrum row is still
 // stored (the caller's spectrum buffer is an output of pv_process), but it is
 // never read back: per frame 4 hop_a + 8 (N/2+1) + 4 hop_s bytes instead of the split
-// path's 4 hop_a + 16 (N/2+1) + 4 hop_s, and one launch instead of two (config 2 is a
-// single stream: per-launch costs, not bytes, bound it).
+// path's 4 hop_a + 16 (N/2+1) + 4 hop_s, and one launch instead of two.  Config 2, a
+// single stream, runs as one round of 3445 waves that is bound by the issue of the SIMDs
+// holding 4 of them, not by bytes (per-wave stamps).
 //
 // The per-frame arithmetic is k_std_analysis's (window, FFT, split, atan2, sqrt) and
 // k_synthesis's (synth_frame, register overlap-add, tails, seams) operation for operation,
