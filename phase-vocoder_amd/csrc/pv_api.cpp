@@ -91,7 +91,13 @@ struct Profile {
     int stride = 1;        // time every stride-th pv_analysis / pv_resynthesis / pv_process call
     long long calls = 0;
     bool active = true;    // this call's launches are timed
+    // consecutive launches of one call share an event: launch i's stop is launch i+1's start
+    // (nothing else is enqueued between them), one event record per launch instead of two
+    bool chain_ok = false;
+    hipEvent_t chain_ev = nullptr;
+    hipStream_t chain_s = nullptr;
     std::vector<hipEvent_t> ev_start, ev_stop;
+    std::vector<char> ev_shared;   // ev_start[i] is ev_stop[i-1] (returned to the pool once)
     std::vector<hipEvent_t> pool;  // read-out events, reused (hipEventCreate per launch costs µs)
     std::vector<int> ev_kernel;
     double total_ms[kNumKernels] = {0};
@@ -154,6 +160,18 @@ void prof_tick(pv_handle* h) {
     if (h->prof.enabled) h->prof.active = (h->prof.calls++ % h->prof.stride) == 0;
 }
 
+// the launches of one pv_analysis / pv_resynthesis / pv_process call, which enqueue nothing
+// but kernels, may chain their events
+struct ProfCall {
+    pv_handle* h;
+    explicit ProfCall(pv_handle* hh) : h(hh) {
+        prof_tick(h);
+        h->prof.chain_ok = true;
+        h->prof.chain_ev = nullptr;
+    }
+    ~ProfCall() { h->prof.chain_ok = false; h->prof.chain_ev = nullptr; }
+};
+
 pv_status prof_begin(pv_handle* h, int kernel, hipStream_t s) {
     if (!h->prof.enabled || !h->prof.active) return PV_OK;
     hipEvent_t a, b;
@@ -166,12 +184,16 @@ pv_status prof_begin(pv_handle* h, int kernel, hipStream_t s) {
         PV_HIP(hipEventCreate(e));
         return PV_OK;
     };
-    pv_status st = take(&a);
+    const bool shared = h->prof.chain_ok && h->prof.chain_ev && h->prof.chain_s == s;
+    pv_status st = PV_OK;
+    if (shared) a = h->prof.chain_ev;
+    else st = take(&a);
     if (st == PV_OK) st = take(&b);
     if (st != PV_OK) return st;
-    PV_HIP(hipEventRecord(a, s));
+    if (!shared) PV_HIP(hipEventRecord(a, s));
     h->prof.ev_start.push_back(a);
     h->prof.ev_stop.push_back(b);
+    h->prof.ev_shared.push_back(shared ? 1 : 0);
     h->prof.ev_kernel.push_back(kernel);
     return PV_OK;
 }
@@ -179,6 +201,10 @@ pv_status prof_begin(pv_handle* h, int kernel, hipStream_t s) {
 pv_status prof_end(pv_handle* h, hipStream_t s) {
     if (!h->prof.enabled || !h->prof.active) return PV_OK;
     PV_HIP(hipEventRecord(h->prof.ev_stop.back(), s));
+    if (h->prof.chain_ok) {
+        h->prof.chain_ev = h->prof.ev_stop.back();
+        h->prof.chain_s = s;
+    }
     return PV_OK;
 }
 
@@ -453,7 +479,8 @@ void pv_destroy(pv_handle* h) {
 #ifdef PV_FUSED_STAMPS
     if (h->d_stamps) (void)hipFree(h->d_stamps);
 #endif
-    for (auto e : h->prof.ev_start) (void)hipEventDestroy(e);
+    for (size_t i = 0; i < h->prof.ev_start.size(); ++i)
+        if (!h->prof.ev_shared[i]) (void)hipEventDestroy(h->prof.ev_start[i]);
     for (auto e : h->prof.ev_stop) (void)hipEventDestroy(e);
     for (auto e : h->prof.pool) (void)hipEventDestroy(e);
     delete h;
@@ -694,7 +721,7 @@ pv_status pv_analysis(pv_handle* h, const float* x, long long ldx, long long n_s
     pv_status st = check_common(h, channels, frames);
     if (st != PV_OK) return st;
     DeviceGuard g(h->cfg.device);
-    prof_tick(h);
+    ProfCall pc_(h);
     return do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, false,
                        (hipStream_t)stream);
 }
@@ -705,7 +732,7 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     pv_status st = check_common(h, channels, frames);
     if (st != PV_OK) return st;
     DeviceGuard g(h->cfg.device);
-    prof_tick(h);
+    ProfCall pc_(h);
     return do_resynthesis(h, spec, ld_spec, channels, frames, ola_in, ld_ola, out, ldo, false,
                           (hipStream_t)stream);
 }
@@ -716,7 +743,7 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     pv_status st = check_common(h, channels, frames);
     if (st != PV_OK) return st;
     DeviceGuard g(h->cfg.device);
-    prof_tick(h);
+    ProfCall pc_(h);
     hipStream_t s = (hipStream_t)stream;
     if (h->F_fused > 0) return do_fused(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
@@ -865,12 +892,14 @@ int pv_profile_read(pv_handle* h, const char** names, double* total_ms, int* lau
             h->prof.total_ms[h->prof.ev_kernel[i]] += ms;
             h->prof.launches[h->prof.ev_kernel[i]] += 1;
         }
-        h->prof.pool.push_back(h->prof.ev_start[i]);
+        if (!h->prof.ev_shared[i]) h->prof.pool.push_back(h->prof.ev_start[i]);
         h->prof.pool.push_back(h->prof.ev_stop[i]);
     }
     h->prof.ev_start.clear();
     h->prof.ev_stop.clear();
+    h->prof.ev_shared.clear();
     h->prof.ev_kernel.clear();
+    h->prof.chain_ev = nullptr;
     int n = 0;
     for (int k = 0; k < kNumKernels && n < cap; ++k) {
         if (h->prof.launches[k] == 0) continue;
