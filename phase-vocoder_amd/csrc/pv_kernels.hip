@@ -215,6 +215,49 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (
         for (int s = 0; s < NS - D; ++s) r2[64 * s + lane] = acc[s];
     }
     __syncthreads();
+    const int nwg = (p.nruns + 3) / 4;
+    const bool last = (blockIdx.x + 1 >= nwg);
+    if constexpr (ROLA && N > 128 * DT) {
+        if (p.out_aligned) {
+            // the overlap is TM = (N - 128 DT) / 128 float2 per lane at positions 2 lane +
+            // 128 m; positions are even and out_len is even, so a pair is wholly inside out
+            // or wholly past it.  The head read-back is one batch of loads and one wait (per
+            // 64 samples, a load-add-store was one serialized round trip: 14 at config 3)
+            constexpr int TM = (N - 128 * DT) / 128;
+            const float2* own2 = reinterpret_cast<const float2*>(ring) + lane;
+            if (w > 0) {
+                const float2* prev2 = reinterpret_cast<const float2*>(rings + (w - 1) * N) + lane;
+                f2v hd[TM];
+#pragma unroll
+                for (int m = 0; m < TM; ++m) {
+                    const long long gp = obase + 2 * lane + 128 * m;
+                    hd[m] = (gp < p.out_len) ? *reinterpret_cast<const f2v*>(outc + gp) : f2v{0.0f, 0.0f};
+                }
+#pragma unroll
+                for (int m = 0; m < TM; ++m) {
+                    const long long gp = obase + 2 * lane + 128 * m;
+                    const float2 t = prev2[64 * m];
+                    if (gp < p.out_len)
+                        __builtin_nontemporal_store(f2v{hd[m].x + t.x, hd[m].y + t.y}, reinterpret_cast<f2v*>(outc + gp));
+                }
+            }
+            if (w == 3) {
+                const long long nb = obase + (long long)p.F * hs + 2 * lane;
+                float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len + 2 * lane;
+#pragma unroll
+                for (int m = 0; m < TM; ++m) {
+                    const float2 v = own2[64 * m];
+                    if (last) {
+                        if (nb + 128 * m < p.out_len)
+                            __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(outc + nb + 128 * m));
+                    } else {
+                        *reinterpret_cast<f2v*>(tdst + 128 * m) = f2v{v.x, v.y};
+                    }
+                }
+            }
+            return;
+        }
+    }
     // seams: run w's tail (positions F*hs + j) overlaps run w+1's head
     if (w > 0) {
         const float* prev = rings + (w - 1) * N;
@@ -224,8 +267,6 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (
         }
     }
     if (w == 3) {
-        const int nwg = (p.nruns + 3) / 4;
-        const bool last = (blockIdx.x + 1 >= nwg);
         float* tdst = p.tails + ((long long)c * nwg + blockIdx.x) * p.tail_len;
         for (int j = lane; j < TL; j += 64) {
             const float v = ring[ROLA ? j : ((p.F * hs + j) & (N - 1))];
