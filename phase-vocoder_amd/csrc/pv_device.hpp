@@ -452,6 +452,20 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
 #pragma unroll
         for (int st = 0; st < r; ++st) {
             const int Ns = S << st;
+            // the stage's 2^st distinct LDS twiddles, read once and as one batch before its
+            // butterflies: R / 2 butterflies share them (the LDS loads are volatile, so a
+            // per-butterfly read was never merged: at L = 1024 32 serialized round trips per
+            // pass instead of 15 batched ones)
+            constexpr bool LDS_TW = (P > 0);
+            float2 wst[R / 2];
+            if constexpr (LDS_TW) {
+                if (Ns > 2) {
+#pragma unroll
+                    for (int bb = 0; bb < (1 << st); ++bb)
+                        wst[bb] = (TWS_MIN > 0 && Ns >= TWS_MIN) ? lds_ld(&tws[(jm + S * bb) * (L / Ns)])
+                                                                 : lds_ld(&tw[(Ns - 1) + jm + S * bb]);
+                }
+            }
             f2v b[R];
 #pragma unroll
             for (int s = 0; s < R / 2; ++s) {
@@ -484,8 +498,7 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                     const float2 w = tw0[(Ns - 1) + br];
                     t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
                 } else {
-                    const float2 w = (TWS_MIN > 0 && Ns >= TWS_MIN) ? lds_ld(&tws[(jm + S * br) * (L / Ns)])
-                                                                    : lds_ld(&tw[(Ns - 1) + jm + S * br]);
+                    const float2 w = wst[br];
                     t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
                 }
                 b[2 * s] = top + t;
