@@ -337,6 +337,11 @@ __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) 
 // instructions in issue order, so a cross-lane exchange (ds_write by lane a, later
 // ds_read by lane b) needs no s_waitcnt: only the compiler must keep program order,
 // which the memory clobber enforces.
+// s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: vmcnt [3:0] and [15:14] = 0,
+// expcnt [6:4] = 7 and lgkmcnt [11:8] = 15 mean "no wait"); as a builtin, unlike inline asm,
+// the compiler's wait insertion sees it
+constexpr int kVmcnt0 = 0x0F70;
+
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("" ::: "memory");
 }

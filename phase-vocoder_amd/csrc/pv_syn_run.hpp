@@ -381,6 +381,8 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
             vm_wait<D>(ra);
         }
     } else {
+        const bool fast_st = ROLA && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
+        (void)fast_st;
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
         auto load_row = [&](const float2* srow) {
             PV_FOR_BINS(E, lane, {
@@ -400,6 +402,10 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
                 synth(u, t, cur, z);
                 if constexpr (ROLA) {
                     ola_regs(z);
+                    // the next row has had the whole frame to land: wait for it here, before
+                    // the frame's output stores, so the compiler's wait for the row's
+                    // registers at the loop edge does not also wait for those stores
+                    __builtin_amdgcn_s_waitcnt(kVmcnt0);
                 } else {
                     // overlap-add the frame into the ring (lane-distinct positions)
                     // y[nn], nn = (n + ROT) mod N, n = lane + 64 i: float index
@@ -419,7 +425,12 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
                 }
             }
             if constexpr (ROLA) {
-                flush_regs(u, std::false_type{});
+                // a run whose stores are all in bounds takes the unconditional stores
+                // (wave-uniform test): per-lane bounds-checked stores sit in exec-masked
+                // blocks, after which the compiler waits for every store of the frame
+                // (vmcnt(0)) before the next row's registers may be moved
+                if (fast_st) flush_regs(u, std::true_type{});
+                else flush_regs(u, std::false_type{});
             } else {
                 // positions [u*hs, (u+1)*hs) are final for this run
                 for (int j = lane; j < hs; j += 64) {
