@@ -293,21 +293,36 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             // by bin every map read -> tile read pair would be two serialized LDS round trips
             // per bin (34 per frame at L = 1024).
             // (config 4 synthesis -2.5 %; 1 at L <= 512, whose kernels sit at their VGPR budget)
+            // At L >= 1024 the groups are software-pipelined: group g + 1's map reads are
+            // issued right after group g's tile reads, so they are in flight while group g
+            // computes and one LDS round trip per group is exposed instead of two.
             constexpr int G = (L >= 1024) ? 4 : 1;
+            constexpr int NGRP = (E + G) / G;
+            auto map_reads = [&](auto ig, i2v (&sc)[G]) {
+                constexpr int i0 = decltype(ig)::value * G;
+                static_for<0, G>([&](auto jj) {
+                    constexpr int j = decltype(jj)::value;
+                    constexpr int i = i0 + j;
+                    if constexpr (i <= E) {
+                        const int k = (i == E) ? L : lane + 64 * i;
+                        if (i < E || lane == 0) sc[j] = lds_ld2i(&srcl[2 * k]);
+                    }
+                });
+            };
             auto gather = [&](auto multi_tag) {
                 constexpr bool MULTI = decltype(multi_tag)::value;
-                static_for<0, (E + G) / G>([&](auto ig) {
+                i2v scn[G];  // the next group's map entries (in flight)
+                if constexpr (L >= 1024) map_reads(std::integral_constant<int, 0>{}, scn);
+                static_for<0, NGRP>([&](auto ig) {
                     constexpr int i0 = decltype(ig)::value * G;
                     i2v sc[G];
                     float2 f[G];
-                    static_for<0, G>([&](auto jj) {
-                        constexpr int j = decltype(jj)::value;
-                        constexpr int i = i0 + j;
-                        if constexpr (i <= E) {
-                            const int k = (i == E) ? L : lane + 64 * i;
-                            if (i < E || lane == 0) sc[j] = lds_ld2i(&srcl[2 * k]);
-                        }
-                    });
+                    if constexpr (L >= 1024) {
+#pragma unroll
+                        for (int j = 0; j < G; ++j) sc[j] = scn[j];
+                    } else {
+                        map_reads(ig, sc);
+                    }
                     static_for<0, G>([&](auto jj) {
                         constexpr int j = decltype(jj)::value;
                         constexpr int i = i0 + j;
@@ -316,6 +331,8 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                             if (i < E || lane == 0) f[j] = lds_ld(&tile[G_::pad(sidx >= 0 ? sidx : 0)]);
                         }
                     });
+                    if constexpr (L >= 1024 && decltype(ig)::value + 1 < NGRP)
+                        map_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, scn);
                     static_for<0, G>([&](auto jj) {
                         constexpr int j = decltype(jj)::value;
                         constexpr int i = i0 + j;
