@@ -445,32 +445,38 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
     constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
     constexpr int R = 1 << r;
     constexpr int NG = G_::E / R;
+    constexpr int E = G_::E;
+    // the stages run on native 2-vectors (64-bit register pairs), so the packed operations
+    // need no register moves to assemble their operands.  Stage-major over the NG groups of
+    // R points: a stage's LDS twiddles for every group (2^st distinct per group: R / 2
+    // butterflies share them) are read once, as one batch, before its butterflies — at most
+    // 8 per batch, else group by group.  The LDS loads are volatile, so per-butterfly reads
+    // were never merged (at L = 1024: 32 serialized round trips in pass 1 and 8 in pass 2
+    // instead of 4 and 2 batched ones).  Each group's operations are unchanged.
+    f2v a[E];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        const int j = lane + 64 * g;
-        const int jm = j & (S - 1);
-        // the stages run on native 2-vectors (64-bit register pairs), so the packed
-        // operations need no register moves to assemble their operands
-        f2v a[R];
+    for (int q = 0; q < E; ++q) a[q] = f2v{v[q].x, v[q].y};
 #pragma unroll
-        for (int q = 0; q < R; ++q) a[q] = f2v{v[g * R + q].x, v[g * R + q].y};
+    for (int st = 0; st < r; ++st) {
+        const int Ns = S << st;
+        const bool lds_tw = (P > 0) && Ns > 2;
+        const bool batch_all = NG * (1 << st) <= 8;
+        float2 wst[NG][R / 2];
+        auto load_tw = [&](int g) {
+            const int jm = (lane + 64 * g) & (S - 1);
 #pragma unroll
-        for (int st = 0; st < r; ++st) {
-            const int Ns = S << st;
-            // the stage's 2^st distinct LDS twiddles, read once and as one batch before its
-            // butterflies: R / 2 butterflies share them (the LDS loads are volatile, so a
-            // per-butterfly read was never merged: at L = 1024 32 serialized round trips per
-            // pass instead of 15 batched ones)
-            constexpr bool LDS_TW = (P > 0);
-            float2 wst[R / 2];
-            if constexpr (LDS_TW) {
-                if (Ns > 2) {
+            for (int bb = 0; bb < (1 << st); ++bb)
+                wst[g][bb] = (TWS_MIN > 0 && Ns >= TWS_MIN) ? lds_ld(&tws[(jm + S * bb) * (L / Ns)])
+                                                             : lds_ld(&tw[(Ns - 1) + jm + S * bb]);
+        };
+        if (lds_tw && batch_all) {
 #pragma unroll
-                    for (int bb = 0; bb < (1 << st); ++bb)
-                        wst[bb] = (TWS_MIN > 0 && Ns >= TWS_MIN) ? lds_ld(&tws[(jm + S * bb) * (L / Ns)])
-                                                                 : lds_ld(&tw[(Ns - 1) + jm + S * bb]);
-                }
-            }
+            for (int g = 0; g < NG; ++g) load_tw(g);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int jm = (lane + 64 * g) & (S - 1);
+            if (lds_tw && !batch_all) load_tw(g);
             f2v b[R];
 #pragma unroll
             for (int s = 0; s < R / 2; ++s) {
@@ -478,8 +484,8 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                 // pass 0: jm = 0, S = 1: compile-time index into the hoisted tw0 (SGPRs)
                 // packed (v_pk_*) form of cmul + butterfly, same roundings as cmul();
                 // INV multiplies by conj(w)
-                const f2v top = a[s];
-                const f2v bot = a[s + R / 2];
+                const f2v top = a[g * R + s];
+                const f2v bot = a[g * R + s + R / 2];
                 if (P == 0 && Ns == 2 && br != 0) {  // compile-time in pass 0
                     // W = exactly -i (+i when INV): top +- (bot.y, -bot.x) as two packed adds
                     // whose op_sel / neg modifiers swap and negate bot (no register moves)
@@ -497,24 +503,24 @@ __device__ __forceinline__ void fft_pass(float2 (&v)[Geo<L>::E], const float2* t
                     t = bot;  // W = 1 exactly (fp32 contract)
                 } else if (Ns == 2) {
                     // later pass (L = 128): W = 1 or exactly -i (+i when INV) by lane
-                    const f2v r = INV ? f2v{-bot.y, bot.x} : f2v{bot.y, -bot.x};
-                    t = (jm != 0) ? r : bot;
+                    const f2v rr = INV ? f2v{-bot.y, bot.x} : f2v{bot.y, -bot.x};
+                    t = (jm != 0) ? rr : bot;
                 } else if constexpr (P == 0) {
                     const float2 w = tw0[(Ns - 1) + br];
                     t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
                 } else {
-                    const float2 w = wst[br];
+                    const float2 w = wst[g][br];
                     t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
                 }
                 b[2 * s] = top + t;
                 b[2 * s + 1] = top - t;
             }
 #pragma unroll
-            for (int q = 0; q < R; ++q) a[q] = b[q];
+            for (int q = 0; q < R; ++q) a[g * R + q] = b[q];
         }
-#pragma unroll
-        for (int q = 0; q < R; ++q) v[g * R + q] = make_float2(a[q].x, a[q].y);
     }
+#pragma unroll
+    for (int q = 0; q < E; ++q) v[q] = make_float2(a[q].x, a[q].y);
 }
 
 template <int L, int P>
