@@ -39,13 +39,14 @@ struct AnaLds {
 template <int E, bool PACKED>
 constexpr int row_stores() { return PACKED ? E : E + 1; }
 
-// One wave = one run of frames t0 .. t0 + nfr - 1 of channel c.  The frame t0 - 1 (halo)
-// is transformed too (phase only) to seed phprev, so the run's first decision m0 = m(t0)
-// is known here and goes to the run record.  On return phprev = phi of the run's last
-// frame and sacc = -(sum of the decisions of frames t0 + 1 .. t0 + nfr - 1) as exact small
-// integers in fp32.  Rows go out with non-temporal stores (they are read back by another
-// launch, long after they would have left the caches).  rec (nullable): the run record
-// {S, m0}.
+// One wave = one run of frames t0 .. t0 + nfr - 1 of channel c.  The run's first decision
+// m0 = m(t0) needs phi(t0 - 1), the previous run's last frame: it is not recomputed here (no
+// halo frame) but made by k_carry from the two runs' records.  On return phprev = phi of the
+// run's last frame and sacc = -(sum of the decisions of frames t0 + 1 .. t0 + nfr - 1) as
+// exact small integers in fp32.  Rows go out with non-temporal stores (they are read back by
+// another launch, long after they would have left the caches).  rec (nullable): the run
+// record {S, phi(t0), phi(t0 + nfr - 1)} (kRecFields rows of bins_pad words, phases as their
+// float bits).
 template <int L, bool EKL, int D, bool PACKED>
 __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
@@ -63,12 +64,13 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     const float* winl = lt.winl;
     const float* ekl = lt.ekl;
     (void)ekl;
+    // e_k of bin L (with per-lane constants, lane 0's: L is a multiple of 64)
+    const float e_L = EKL ? lds_ld(&ekl[L]) : __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(e_lane)));
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
     PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0.0f; })
 
-    // One frame: window + FFT + split + atan2 (+ spectrum row, decisions) from raw samples.
-    // IS_HALO (frame t0 - 1): phase only, it seeds phprev.
+    // One frame: window + FFT + split + atan2, spectrum row, decisions, from raw samples.
     auto window = [&](const float2 (&xr)[E], float2 (&z)[E]) {
         const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
 #pragma unroll
@@ -78,72 +80,73 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             z[q].y = xr[q].y * wv.y;
         }
     };
-    auto frame = [&](int u, float2 (&z)[E], auto halo_tag) {
-        constexpr bool IS_HALO = decltype(halo_tag)::value;
+    auto frame = [&](int u, float2 (&z)[E]) {
         float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
         (void)srow;
         // the last pass's registers feed the split directly (no final image in LDS)
         fft_run<L, false, false, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
-        [[maybe_unused]] float mag0 = 0.0f, ph0 = 0.0f;  // packed: bin `lane` until slot 0 goes out
-        // bins in chunks of CH (bounded live registers), all reads of a chunk batched; both
-        // layouts take bins in the order 0, L, 1 .. E-1 (bin_at<E, true>): in natural order
-        // the L = 1024 natural-row kernels spill 1-2 VGPRs at 168 (3 waves/SIMD), which the
-        // self-tracked prefetch must never see (tests/test_abi.py)
-        static_for<0, (E + CH) / CH>([&](auto ic) {
+        // bin L first (the packed slot 0 pairs it with bin 0): it is real, so its contract
+        // phase is +0 or pi and needs no atan2 — computed once, wave-uniformly, instead of as
+        // a ninth generic bin on every lane (bin_l_real)
+        float magL, phL;
+        bin_l_real<L, true>(z, twsl, magL, phL);
+        // bin L's decision (wave-uniform; lane 0's copy is the one recorded).  Frame t0's
+        // decision is against phprev = 0, not phi(t0 - 1): it is taken back out of S at once
+        // (wave-uniform branch, once per run) and the phase goes to the record instead.
+        {
+            const float mr = unwrap_round(phL, phprev[E], e_L);
+            sacc[E] += mr;
+            if (u == 0) {
+                sacc[E] -= mr;
+                if (rec != nullptr && lane == 0) rec[BP + L] = __float_as_int(phL);
+            }
+        }
+        phprev[E] = phL;
+        // bins 0 .. E-1 of the lane in chunks of CH (bounded live registers), all reads of a
+        // chunk batched, phases of each pair through the packed atan2
+        static_for<0, E / CH>([&](auto ic) {
             constexpr int p0 = decltype(ic)::value * CH;
             float2 X[CH];
-            split_chunk_bp<L, CH, true, p0, true>(z, twsl, lane, X);
-            // phases of the chunk's bins: pairs through the packed atan2
+            split_chunk_bp<L, CH, true, p0, false>(z, twsl, lane, X);
             float phs[CH];
             static_for<0, CH / 2>([&](auto jj) {
                 constexpr int j = 2 * decltype(jj)::value;
-                if constexpr (p0 + j + 1 <= E) {
-                    const f2v ph2 = atan2_pv2(X[j].y, X[j].x, X[j + 1].y, X[j + 1].x);
-                    phs[j] = ph2.x;
-                    phs[j + 1] = ph2.y;
-                } else if constexpr (p0 + j <= E) {
-                    phs[j] = atan2_pv(X[j].y, X[j].x);
-                }
+                const f2v ph2 = atan2_pv2(X[j].y, X[j].x, X[j + 1].y, X[j + 1].x);
+                phs[j] = ph2.x;
+                phs[j + 1] = ph2.y;
             });
-            if constexpr (CH % 2 == 1 && p0 + CH - 1 <= E) phs[CH - 1] = atan2_pv(X[CH - 1].y, X[CH - 1].x);
             static_for<0, CH>([&](auto cc) {
                 constexpr int c2 = decltype(cc)::value;
-                if constexpr (p0 + c2 <= E) {
-                    constexpr int i = bin_at<E, true>(p0 + c2);
-                    const int k = (i == E) ? L : lane + 64 * i;
-                    (void)k;
-                    const float ph = phs[c2];
-                    if constexpr (!IS_HALO) {
-                        // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
-                        // the phase, which drives the unwrap decisions, stays bit-exact.  X
-                        // came out doubled (split_chunk_bp TWICE): halve the magnitude.
-                        const float mag = 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
-                        if constexpr (!PACKED) {
-                            // bin L (i = E) has the same value and address on every lane
-                            __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
-                        } else if constexpr (i == 0) {
-                            mag0 = mag;
-                            ph0 = ph;
-                        } else if constexpr (i == E) {
-                            // slot 0: lane 0 carries bins 0 and L (both real), the others bin lane
-                            const f2v s0 = (lane == 0) ? f2v{pack_real_bin(mag0, ph0), pack_real_bin(mag, ph)}
-                                                       : f2v{mag0, ph0};
-                            __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
-                        } else {
-                            __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
-                        }
-                        // m = -mr; the run's first decision is the record's m0, not part of
-                        // S: it is subtracted like every other and added back in the
-                        // (wave-uniform, once per run) u == 0 branch
-                        const float mr = unwrap_round(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
-                        sacc[i] += mr;
-                        if (u == 0) {
-                            sacc[i] -= mr;
-                            if (rec != nullptr && (i < E || lane == 0)) rec[BP + k] = -(int)mr;
-                        }
+                constexpr int i = p0 + c2;
+                const int k = lane + 64 * i;
+                (void)k;
+                const float ph = phs[c2];
+                {
+                    // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
+                    // the phase, which drives the unwrap decisions, stays bit-exact.  X
+                    // came out doubled (split_chunk_bp TWICE): halve the magnitude.
+                    const float mag = 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    if constexpr (PACKED && i == 0) {
+                        // slot 0: lane 0 carries bins 0 and L (both real), the others bin lane
+                        const f2v s0 = (lane == 0) ? f2v{pack_real_bin(mag, ph), pack_real_bin(magL, phL)}
+                                                   : f2v{mag, ph};
+                        __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+                    } else {
+                        __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
                     }
-                    phprev[i] = ph;
+                    if constexpr (!PACKED && i == 0) {
+                        // bin L: the same value and address on every lane
+                        __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
+                    }
+                    // m = -mr (frame t0: as bin L above)
+                    const float mr = unwrap_round(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
+                    sacc[i] += mr;
+                    if (u == 0) {
+                        sacc[i] -= mr;
+                        if (rec != nullptr) rec[BP + k] = __float_as_int(ph);
+                    }
                 }
+                phprev[i] = ph;
             });
         });
         wave_lds_sync();  // tile reads done before the next frame's pass_store
@@ -167,12 +170,6 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     // last frame fully inside: floor((n - N) / hop), -1 when n < N (C++ division truncates
     // toward zero, which for N - hop < n < N would give 0 and read frame 0 past the end)
     const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
-    if (t0 > 0) {
-        float2 xh[E], z[E];
-        if (t0 - 1 <= lastfull) load_fast(-1, xh); else load_checked(-1, xh);
-        window(xh, z);
-        frame(-1, z, std::true_type{});
-    }
     const int ufast = (int)min((long long)nfr, max(0LL, lastfull - t0 + 1));
     // steady state, trip u: [load x(u+1)] [compute frame u: NST row stores]
     // [vmcnt(NST): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
@@ -187,7 +184,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             for (int u = 0; u < ufast; ++u) {
                 f2v xv[D];  // the D new pairs of frame u+1: registers E-D .. E-1
                 gload_tail<D, E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
-                frame(u, z, std::false_type{});  // exactly NST row stores (+ records at u = 0)
+                frame(u, z);  // exactly NST row stores (+ records at u = 0)
                 vm_wait<NST>(xv);
 #pragma unroll
                 for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
@@ -206,7 +203,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         for (int u = 0; u < ufast; ++u) {
             f2v xv[E];
             gload_pairs<E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
-            frame(u, z, std::false_type{});  // exactly NST row stores
+            frame(u, z);  // exactly NST row stores
             vm_wait<NST>(xv);
             float2 xr[E];
 #pragma unroll
@@ -220,16 +217,16 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             float2 z[E];
             window(xr, z);
             load_fast(min(u + 1, ufast - 1), xr);
-            frame(u, z, std::false_type{});
+            frame(u, z);
         }
     }
     for (int u = ufast; u < nfr; ++u) {
         float2 xr[E], z[E];
         load_checked(u, xr);
         window(xr, z);
-        frame(u, z, std::false_type{});
+        frame(u, z);
     }
-    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = -(int)sacc[i]; })
+    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = -(int)sacc[i]; rec[2 * BP + k] = __float_as_int(phprev[i]); })
 }
 
 }  // namespace pv

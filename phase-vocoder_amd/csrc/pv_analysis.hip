@@ -8,9 +8,10 @@
 namespace pv {
 
 // ------------------------------------------------------------------ K1 STANDARD
-// One wave = one run of F consecutive frames (plus the halo frame t0-1, transformed only
-// for its phase).  The unwrap decision m(t) = f(phi[t], phi[t-1]) is accumulated in
-// registers: S = sum over t in (t0, t0+F) and m0 = m(t0) go to the run record.
+// One wave = one run of F consecutive frames.  The unwrap decision m(t) = f(phi[t],
+// phi[t-1]) is accumulated in registers: S = sum over t in (t0, t0+F), phi(t0) and phi of the
+// run's last frame go to the run record (k_carry makes m(t0) from them and the previous run's
+// record).
 // EKL: the expected advance e_k from an LDS table; otherwise (64 a multiple of the hop
 // divisor, so e_k depends on k mod 64 only) one register per lane, e_k = ek[lane].
 // waves per SIMD the analysis is compiled for (__launch_bounds__): L = 512 at <= 128 VGPRs
@@ -51,9 +52,9 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L
     if (run >= p.nruns) return;
     const int t0 = run * p.F;
     const int nfr = min(p.F, p.frames - t0);
-    // run record {S, m0}: m0 (the decision of the run's first frame) is stored as soon as
-    // it is known, S after the loop
-    int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * 2 * p.bins_pad : nullptr;
+    // run record {S, phi(t0), phi(last)}: phi(t0) is stored as soon as it is known, the rest
+    // after the loop
+    int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad : nullptr;
     float phprev[E + 1], sacc[E + 1];
     ana_run<L, EKL, D, PACKED>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c, t0, nfr,
                                e_lane, rec, phprev, sacc);

@@ -695,7 +695,7 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     const size_t runs_total = chans * std::max(h->max_runs, 1);
     const size_t wg_total = chans * std::max((std::max(h->max_runs, runs_fused) + 3) / 4, 1);
     if (h->mode == PV_MODE_STANDARD) {
-        PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * 2 * h->bins_pad));
+        PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * pv::kRecFields * h->bins_pad));
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
     }
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));

@@ -136,6 +136,31 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
     });
 }
 
+// Bin L of the real split, wave-uniform: A = B = Z[0] (lane 0's slot 0, broadcast), the same
+// operations as split_chunk_bp's bin L, then {magnitude, contract phase} of a real bin.  With
+// Im X = +0 the contract's atan2_pv(+0, X) has a = 0, so the polynomial gives +0 and only the
+// x < 0 fix-up applies: pi for X < 0, +0 otherwise (X = -0 included) — bit for bit the generic
+// bin's phase, without its reciprocal, polynomial and octant fix-ups.  The magnitude is the
+// generic bin's formula (Im^2 = +0).  TWICE: X scaled by 2 as in split_chunk_bp (the caller's
+// magnitude is halved here too, so magL is the contract's |X|).
+template <int L, bool TWICE>
+__device__ __forceinline__ void bin_l_real(const float2 (&v)[Geo<L>::E], const float2* twsl, float& magL,
+                                           float& phL) {
+    const float2 z0 = v[slot_reg<L>(0)];
+    const float ax = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z0.x)));
+    const float ay = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z0.y)));
+    const float2 tw = lds_ld(&twsl[L]);
+    constexpr float h = TWICE ? 1.0f : 0.5f;
+    const float er = h * (ax + ax);
+    const float orr = h * (ay + ay);
+    const float oi = h * (ax - ax);
+    const float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
+    const float zero = 0.0f;
+    const float m = __builtin_amdgcn_sqrtf(__builtin_fmaf(Xr, Xr, zero * zero));
+    magL = TWICE ? 0.5f * m : m;
+    phL = (Xr < 0.0f) ? kPi : 0.0f;
+}
+
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
 #define PV_FOR_BINS(E_, lane_, ...)                              \
     _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \

@@ -5,6 +5,12 @@
 
 namespace pv {
 
+// STANDARD run record per (channel, run): kRecFields rows of bins_pad int32 words —
+// S = sum of the unwrap decisions of the run's frames after its first, then phi of the run's
+// first and of its last frame (float bits).  k_carry makes the first frame's decision from
+// phi(t0) and the previous run's last phase.
+constexpr int kRecFields = 3;
+
 struct AnaParams {
     const float* x;
     long long ldx, n;
@@ -18,7 +24,7 @@ struct AnaParams {
     float2* spec;
     long long ld_spec;
     int spec_stride;
-    int* runsum;            // [C][nruns][2][bins_pad] {S, m0} or nullptr
+    int* runsum;            // [C][nruns][kRecFields][bins_pad] run records or nullptr
     int bins_pad;
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
     int packed;             // STANDARD rows in the PV_SPEC_PACKED layout (bin L in slot 0)

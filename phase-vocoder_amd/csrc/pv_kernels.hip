@@ -17,8 +17,8 @@
 namespace pv {
 
 // ------------------------------------------------------------------ K2 scans
-// run record from an existing spectrum (pv_resynthesis path): S (pairs inside the run)
-// and m0 = m(t0) against phi[t0-1] (0 before the first frame).
+// run record from an existing spectrum (pv_resynthesis path), the layout K1 writes
+// (kRecFields): S = the decisions of the frames after the run's first, phi(t0), phi(last).
 __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int run = blockIdx.y, c = blockIdx.z;
@@ -34,22 +34,23 @@ __global__ __launch_bounds__(256) void k_runsum(ScanParams p) {
         return (__float_as_uint(k == 0 ? v.x : v.y) >> 31) ? kPi : 0.0f;
     };
     const float e = p.ek[k];
-    float prev = (t0 > 0) ? phase(-1) : 0.0f;
-    float ph = phase(0);
-    const int m0 = unwrap_count(ph, prev, e);
-    prev = ph;
+    const float ph0 = phase(0);
+    float prev = ph0;
     int acc = 0;
     for (int u = 1; u < nfr; ++u) {
-        ph = phase(u);
+        const float ph = phase(u);
         acc += unwrap_count(ph, prev, e);
         prev = ph;
     }
-    int* dst = p.runsum + ((long long)c * p.nruns + run) * 2 * p.bins_pad;
+    int* dst = p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad;
     dst[k] = acc;
-    dst[p.bins_pad + k] = m0;
+    dst[p.bins_pad + k] = __float_as_int(ph0);
+    dst[2 * p.bins_pad + k] = __float_as_int(prev);
 }
 
-// carry[run] = M(t0) = sum over earlier runs of (m0 + S) + m0(run).
+// carry[run] = M(t0) = sum over earlier runs of (m0 + S) + m0(run), where m0(run) = m(t0) is
+// the decision of the run's first frame, made here from its record's phi(t0) and the previous
+// run's phi(last) (phi(-1) = 0): the same operations as K1's decisions (unwrap_count).
 // Block = 64 bins x SEG run segments (one wave each): pass 1 sums each segment, the
 // segment offsets are scanned in LDS, pass 2 rescans the segment writing carries.  All
 // integer, so the split of the scan changes no bit.
@@ -61,50 +62,70 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
     const int k = blockIdx.x * 64 + lane;
     const int c = blockIdx.y;
     const int BP = p.bins_pad;
+    constexpr int RF = kRecFields;
     const int per = (p.nruns + SEG - 1) / SEG;
     const int r0 = min(p.nruns, sg * per), r1 = min(p.nruns, r0 + per);
     const bool on = k <= p.L;
-    const int* rs = p.runsum + (long long)c * p.nruns * 2 * BP + (on ? k : 0);
+    const int* rs = p.runsum + (long long)c * p.nruns * RF * BP + (on ? k : 0);
     int* cr = p.carry + (long long)c * p.nruns * BP + (on ? k : 0);
+    const float e = p.ek[on ? k : 0];
+    // S, phi(t0), phi(last) of run r
+    auto S_of = [&](int r) { return rs[(long long)r * RF * BP]; };
+    auto first_of = [&](int r) { return __int_as_float(rs[(long long)r * RF * BP + BP]); };
+    auto last_of = [&](int r) { return __int_as_float(rs[(long long)r * RF * BP + 2 * BP]); };
     int M = 0;
     int run = r0;
     if constexpr (SEG > 1) {  // pass 1 only feeds the other segments' offsets
         int T = 0;
+        float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : 0.0f;
         for (; run + 4 <= r1; run += 4) {
-            int a[8];
+            int sv[4];
+            float fv[4], lv[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                a[2 * j] = rs[(long long)(run + j) * 2 * BP];
-                a[2 * j + 1] = rs[(long long)(run + j) * 2 * BP + BP];
+                sv[j] = S_of(run + j);
+                fv[j] = first_of(run + j);
+                lv[j] = last_of(run + j);
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) T += a[j];
+            for (int j = 0; j < 4; ++j) {
+                T += unwrap_count(fv[j], prev, e) + sv[j];
+                prev = lv[j];
+            }
         }
-        for (; run < r1; ++run) T += rs[(long long)run * 2 * BP] + rs[(long long)run * 2 * BP + BP];
+        for (; run < r1; ++run) {
+            T += unwrap_count(first_of(run), prev, e) + S_of(run);
+            prev = last_of(run);
+        }
         tot[sg][lane] = T;
         __syncthreads();
         for (int j = 0; j < sg; ++j) M += tot[j][lane];
     }
     if (!on) return;
     run = r0;
+    float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : 0.0f;
     for (; run + 4 <= r1; run += 4) {
-        int sv[4], mv[4];
+        int sv[4];
+        float fv[4], lv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            sv[j] = rs[(long long)(run + j) * 2 * BP];
-            mv[j] = rs[(long long)(run + j) * 2 * BP + BP];
+            sv[j] = S_of(run + j);
+            fv[j] = first_of(run + j);
+            lv[j] = last_of(run + j);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            M += mv[j];
+            M += unwrap_count(fv[j], prev, e);
             cr[(long long)(run + j) * BP] = M;
             M += sv[j];
+            prev = lv[j];
         }
     }
     for (; run < r1; ++run) {
-        M += rs[(long long)run * 2 * BP + BP];
+        M += unwrap_count(first_of(run), prev, e);
         cr[(long long)run * BP] = M;
-        M += rs[(long long)run * 2 * BP];
+        M += S_of(run);
+        prev = last_of(run);
     }
 }
 
