@@ -107,13 +107,18 @@ def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, comp
     C_all, n = x.shape
     frames = pvref.num_frames(n, N // hop_div)
     host = f"{threads} threads = this process's CPU share (affinity {aff}, machine {os.cpu_count()})"
+    # REF_COMPAT's checker is an fp64 restatement: slower than an fp32 CPU port of the
+    # reference would be, so the GPU/CPU ratio it gives is overstated (said in the line)
+    note = ("fp64 restatement of kernel.cu / main.cpp, not an fp32 port: an fp32 CPU port would "
+            "be faster, so the GPU/CPU ratio is overstated" if compat else
+            "fp32-contract analysis (the GPU's own phases) + fp64 synthesis")
     if single:
         t0 = time.perf_counter()
         _, used = batch(x[:1], N, hop_div, effect, scale, frames, 1)
         dt = time.perf_counter() - t0
         return {"value": frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
                 "sample": f"the whole stream ({n} samples, {frames} frames) on 1 core, "
-                          f"oracle/pvref.c, {dt:.1f} s wall"}
+                          f"oracle/pvref.c, {dt:.1f} s wall", "note": note}
     k = min(threads, C_all)
     t0 = time.perf_counter()
     _, used = batch(x[:k], N, hop_div, effect, scale, frames, threads)
@@ -127,7 +132,7 @@ def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, comp
     return {"value": C * frames / dt, "unit": "frames/s", "cores": int(used), "kind": "port",
             "sample": f"channels 0..{C - 1} of the GPU batch x {n} samples ({C * frames} frames), "
                       f"{what}, {dt:.1f} s wall; "
-                      f"{host}"}
+                      f"{host}", "note": note}
 
 
 def check_channels(C, k=16):
@@ -178,6 +183,8 @@ def main():
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if args.workload == "rt" and args.gpus > 1:
+        raise SystemExit("bench.py: the real-time workload runs on one GPU (--gpus 1)")
     if "WORLD_SIZE" in os.environ:
         if int(os.environ["WORLD_SIZE"]) != args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
@@ -191,8 +198,6 @@ def main():
     if args.warmup is None:
         args.warmup = 20 if args.workload == "c2" else 3
     if args.workload == "rt":
-        if args.gpus > 1:
-            raise SystemExit("bench.py: the real-time workload runs on one GPU (--gpus 1)")
         return bench_rt(args)
 
     import torch
@@ -303,33 +308,22 @@ def main():
     total_frames = C * frames * world * args.steps
     value = total_frames / dt
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
-    # Spectrum bytes per frame = the row the layout stores: 8 (N/2+1) natural,
-    # 8 N/2 packed (bin N/2 rides in slot 0): the packed figure is the smaller, not inflated
-    # REF_COMPAT writes 2N bins per frame (kernel.cu:337) and its resynthesis reads the
-    # N/2+1 of them its size-N C2R uses (kernel.cu:363-368)
     hop_a, hop_s, B = N // hop_div, pv.outHopSize, pv.spec_bins
-    B_read = N // 2 + 1 if compat else B
-    per_frame = {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
-                 "compat_analysis": 4 * hop_a + 8 * B,
-                 "synthesis": 8 * B_read + 4 * hop_s,    # spectrum read + emitted output
-                 "carry": 0, "runsum": 8 * B, "seam": 0,
-                 # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
-                 "fused": 4 * hop_a + 8 * B + 4 * hop_s}
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     avg_ms = ms_tot / max(launches, 1)
-    alg_bytes = per_frame.get(dom, 0) * C * frames
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            # measured on one workload (config 3 by default): no number for the others
-            if tj.get("_workload", "c3") == wl and tj.get("_layout", "natural") == args.layout:
-                traffic = tj.get(dom, {}).get("bytes_per_launch")
+            # keyed per workload (and spectrum layout): no number for a workload not measured
+            ent = tj.get(wl) if isinstance(tj.get(wl), dict) else (tj if tj.get("_workload", "c3") == wl else None)
+            if ent is not None and ent.get("_layout", "natural") == args.layout:
+                traffic = ent.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
+    roof = roofline(dom, avg_ms, wl, N, hop_a, hop_s, B, C * frames, compat, traffic)
+    achieved = roof["achieved"]
     # the box's measured HBM ceilings: plain streams (scripts/bw_probe.hip ->
     # profiles/r02_bw_probe.jsonl: copy ~6.0, write ~6.0 TB/s against the 8 TB/s spec) and the
     # dominant kernel's own byte mix with no arithmetic, in the product's wave mapping and row
@@ -368,6 +362,7 @@ def main():
                          channels=f"{len(idx)} per rank (indices as rank 0's, rank-local)")
             check["pass"] = bool(t[2] == 0)
             check["all_finite"] = bool(t[3] == 0)
+    B_read = N // 2 + 1 if compat else B
     path_bytes = (4 * hop_a + 4 * hop_s + 8 * B + 8 * B_read) * C * frames * world * args.steps
 
     cpu = None
@@ -391,9 +386,7 @@ def main():
                        "out_hop": hop_s, "spec_layout": args.layout,
                        "parallelism": f"channel-shard x{world}",
                        "dist_backend": backend if distributed else None},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms},
+            "roofline": roof,
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
             "measured_ceiling": ceiling,
             "kernels": kernels,
@@ -407,6 +400,93 @@ def main():
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (dense) peak, MI355X_MICROARCH.md
+SIMDS = 1024               # 256 CUs x 4 SIMDs
+PEAK_SCLK_GHZ = 2.4
+
+
+def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat):
+    """SURVEY §8(d) bytes per frame of each kernel: spectrum row = what the layout stores
+    (8 (N/2+1) natural, 8 N/2 packed: bin N/2 rides in slot 0, the smaller figure);
+    REF_COMPAT writes 2N bins per frame (kernel.cu:337) and its resynthesis reads the N/2+1
+    of them its size-N C2R uses (kernel.cu:363-368)."""
+    B_read = N // 2 + 1 if compat else B
+    return {"analysis": 4 * hop_a + 8 * B,          # new input + spectrum write
+            "compat_analysis": 4 * hop_a + 8 * B,
+            "synthesis": 8 * B_read + 4 * hop_s,    # spectrum read + emitted output
+            "carry": 0, "runsum": 8 * B, "seam": 0,
+            # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
+            "fused": 4 * hop_a + 8 * B + 4 * hop_s}.get(kernel, 0)
+
+
+def alg_flops_per_frame(kernel, N, compat):
+    """SURVEY §8(d) algorithmic flops per frame, split by kernel (the two STANDARD halves sum
+    to 5 N log2 N + 5 N + 40 (N/2+1) = 77 kflop at N = 1024, REF_COMPAT's to 148 kflop):
+      analysis         2.5 N log2 N (real FFT) + N (window) + 25 (N/2+1) (magnitude 3,
+                       atan2 18, unwrap decision 4)
+      compat_analysis  5 (2N) log2 (2N) (C2C 2N, kernel.cu:331) + N + 5 (N/2+1)
+      synthesis        2.5 N log2 N (inverse real FFT) + 4 N (window, gain, overlap-add) +
+                       15 (N/2+1) STANDARD (output phase, sin/cos, polar->rect), 5 (N/2+1)
+                       REF_COMPAT"""
+    lg = math.log2(N)
+    b = N // 2 + 1
+    ana = 2.5 * N * lg + N + 25 * b
+    syn = 2.5 * N * lg + 4 * N + (5 if compat else 15) * b
+    return {"analysis": ana, "compat_analysis": 5 * 2 * N * math.log2(2 * N) + N + 5 * b,
+            "synthesis": syn, "fused": ana + syn}.get(kernel, 0.0)
+
+
+def kernel_sources_sha():
+    """sha256[:16] of the kernel sources, as scripts/isa_static.py records it"""
+    import hashlib
+    d = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".h")):
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
+             isa_path=os.path.join(ROOT, "profiles", "isa_static.json")):
+    """Both roofs of the dominant kernel ("Report both and state which roof
+    binds").  HBM: algorithmic bytes per launch / average launch time against 8 TB/s (the
+    metric's "% HBM roofline": `achieved`, `peak`, `frac`).  VALU: algorithmic flops against
+    the 157.3 TFLOP/s FP32 peak, and the issue-cycle estimate — the kernel's per-frame loop
+    priced at the measured issue cost of each instruction form (scripts/isa_static.py ->
+    profiles/isa_static.json, checked against this build's sources) as a fraction of the
+    SIMD cycles the launch had at the 2.4 GHz peak clock (the chip runs slower under its
+    power cap, so the true busy fraction is higher).  `bound` is the roof with the larger
+    fraction."""
+    t = avg_ms * 1e-3
+    alg_bytes = alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat) * frames
+    achieved = alg_bytes / t / 1e9
+    hbm_frac = achieved / HBM_PEAK_GBS
+    fl = alg_flops_per_frame(kernel, N, compat)
+    tflops = fl * frames / t / 1e12
+    valu = {"flops_per_frame": fl, "achieved_tflops": tflops, "peak_tflops": VALU_PEAK_TFLOPS,
+            "flop_frac": tflops / VALU_PEAK_TFLOPS, "issue_cycles_per_frame": None,
+            "issue_frac_at_peak_clock": None, "issue_source": None}
+    try:
+        isa = json.load(open(isa_path))
+        ent = isa.get(wl, {}).get(kernel)
+        if ent is not None:
+            fresh = isa.get("_sources_sha16") == kernel_sources_sha()
+            cyc = ent["valu_cycles_per_frame"]
+            valu["issue_cycles_per_frame"] = cyc
+            valu["issue_frac_at_peak_clock"] = cyc * frames / (SIMDS * t * PEAK_SCLK_GHZ * 1e9)
+            valu["issue_source"] = ("profiles/isa_static.json (static count of this build's loop, "
+                                    "measured issue costs)" if fresh else
+                                    "profiles/isa_static.json (STALE: sources changed since)")
+    except (OSError, ValueError, KeyError):
+        pass
+    vfrac = max(valu["flop_frac"], valu["issue_frac_at_peak_clock"] or 0.0)
+    return {"bound": "valu" if vfrac > hbm_frac else "hbm", "kernel": kernel,
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
+            "frac_of": "hbm (the metric's % HBM roofline)", "traffic": traffic,
+            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms, "valu": valu}
 
 
 def bench_rt(args):

@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Static VALU issue estimate per frame for the kernels bench.py reports (diagnostic).
+
+Compiles the kernel sources to gfx950 assembly (device only, the Makefile's flags), takes
+each reported kernel's per-frame loop (the smallest loop that holds the frame's LDS
+permutes and global stores) and prices its VALU instructions with the issue costs measured
+on MI355X (cycles per wave-instruction per SIMD at 8 waves/SIMD: profiles/r03_valu_probe2.jsonl,
+profiles/r04_valu_probe3.jsonl).  Writes profiles/isa_static.json, which bench.py turns into
+`roofline.valu.issue_cycles_per_frame` and the issue fraction of the kernel's time.
+
+  python3 scripts/isa_static.py            # -> profiles/isa_static.json
+"""
+import hashlib
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+from collections import Counter
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S"]
+
+# (workload, bench kernel key) -> (source, extra flags, mangled-name prefix, transcendental
+# instructions per frame: the analysis takes E + 1 square roots, the synthesis E + 1 cosines
+# and E sines, E = L / 64 — how many frames one trip of an unrolled loop covers)
+KERNELS = {
+    ("c3", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi512ELb0ELi2ELb1E", 9),
+    ("c3", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi0ELi1ELb1ELb1E", 17),
+    ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1E", 17),
+    ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi2ELi4ELb1ELb1E", 33),
+    ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
+    ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
+}
+
+# issue cycles per wave-instruction at 8 waves/SIMD (measured; see the module docstring)
+FAST = 2.25    # v_fma/fmac/add/sub/mul_f32 (no source modifiers), v_mov_b32, v_add/sub_u32
+SLOW = 4.15    # compares, selects, v_bfi, v_rndne, v_fract, min/max with modifiers, max3, ...
+PACKED = 4.33  # v_pk_fma/mul/add_f32
+TRANS = 8.2    # v_sqrt, v_sin, v_cos, v_rcp, ...
+FAST_OPS = ("v_fma_f32", "v_fmac_f32", "v_fmaak_f32", "v_fmamk_f32", "v_add_f32", "v_sub_f32",
+            "v_subrev_f32", "v_mul_f32", "v_mov_b32", "v_add_u32", "v_sub_u32", "v_subrev_u32")
+FAST_EXTRA = "profiles/r04_valu_costs.json"  # measured overrides {opcode: cycles}, if present
+
+
+def sources_sha():
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".hpp", ".h")):
+            h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def function_body(path, prefix):
+    lines, on = [], False
+    for line in open(path):
+        if not on and re.match(rf"^{re.escape(prefix)}\w*:", line):
+            on = True
+            continue
+        if on:
+            if line.startswith("\t.section") or re.match(r"^\.Lfunc_end", line):
+                break
+            lines.append(line.rstrip("\n"))
+    return lines
+
+
+def cost_of(op, text, extra):
+    if op in extra:
+        return extra[op]
+    if op.startswith(("v_sin", "v_cos", "v_rcp", "v_sqrt", "v_rsq", "v_exp", "v_log")):
+        return TRANS
+    if op.startswith("v_pk_"):
+        return PACKED
+    if op.startswith(FAST_OPS) and "|" not in text and " div:" not in text and " mul:" not in text:
+        return FAST
+    return SLOW
+
+
+def frame_loop(asm, prefix):
+    labels, insts = {}, []
+    for line in function_body(asm, prefix):
+        m = re.match(r"^(\.LBB\w+):", line)
+        if m:
+            labels[m.group(1)] = len(insts)
+            continue
+        s = line.strip()
+        if not s or s.startswith((";", ".")):
+            continue
+        insts.append((s.split()[0], s))
+    best = None
+    for i, (op, s) in enumerate(insts):
+        if op.startswith("s_cbranch") or op == "s_branch":
+            tgt = s.split()[-1]
+            if tgt in labels and labels[tgt] <= i:
+                seg = insts[labels[tgt]:i + 1]
+                ops = [o for o, _ in seg]
+                has_perm = any(o.startswith("ds_bpermute") for o in ops)
+                has_store = any(o.startswith("global_store") for o in ops)
+                if has_perm and has_store and (best is None or len(seg) < len(best)):
+                    best = seg
+    return best
+
+
+def main():
+    extra = {}
+    p = os.path.join(ROOT, FAST_EXTRA)
+    if os.path.exists(p):
+        extra = json.load(open(p)).get("cycles", {})
+    out = {"_sources_sha16": sources_sha(),
+           "_cost_model": {"fast": FAST, "slow": SLOW, "packed": PACKED, "trans": TRANS,
+                           "overrides": FAST_EXTRA if extra else None},
+           "_note": "VALU issue cycles per frame of each kernel's per-frame loop (static, gfx950 "
+                    "assembly of this build), priced at the measured 8-wave issue costs"}
+    cache = {}
+    with tempfile.TemporaryDirectory() as td:
+        for (wl, key), (src, fl, prefix, trans_pf) in KERNELS.items():
+            asm = cache.get((src, tuple(fl)))
+            if asm is None:
+                asm = os.path.join(td, f"{src}{len(cache)}.s")
+                subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *fl, "-o", asm, os.path.join(CSRC, src)],
+                               check=True, stderr=subprocess.DEVNULL)
+                cache[(src, tuple(fl))] = asm
+            seg = frame_loop(asm, prefix)
+            if seg is None:
+                continue
+            cnt = Counter()
+            cyc = 0.0
+            for op, text in seg:
+                if op.startswith("v_"):
+                    c = cost_of(op, text, extra)
+                    cyc += c
+                    cnt["valu_trans" if c == TRANS else "valu_packed" if op.startswith("v_pk_") else "valu"] += 1
+                elif op.startswith("ds_"):
+                    cnt["lds"] += 1
+                elif op.startswith(("global_", "buffer_")):
+                    cnt["vmem"] += 1
+            fpl = max(1, round(cnt["valu_trans"] / trans_pf))  # frames per loop trip
+            out.setdefault(wl, {})[key] = {"symbol": prefix, "loop_instructions": len(seg),
+                                           "frames_per_trip": fpl,
+                                           "counts_per_trip": dict(cnt),
+                                           "valu_cycles_per_frame": round(cyc / fpl, 1)}
+    dst = os.path.join(ROOT, "profiles", "isa_static.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

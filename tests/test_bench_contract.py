@@ -80,3 +80,45 @@ def test_compat_oracle_batch_and_baseline():
     assert chk["pass"] and "compat" in chk["oracle"]
     cpu = bench.cpu_baseline(x, 1024, 4, ord("t"), 1.0, target_s=0.2, compat=True)
     assert cpu["value"] > 0 and "REF_COMPAT" in cpu["sample"]
+
+
+def test_roofline_reports_both_roofs(tmp_path):
+    """the line carries the HBM and the VALU roof of the dominant kernel and
+    names the binding one (`bound`: the larger fraction)."""
+    import json
+    N, hop, hs, B, frames = 1024, 256, 128, 512, 1024 * 1722
+    r = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None)
+    assert r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["achieved"] - (4 * hop + 8 * B) * frames / 2e-3 / 1e9) < 1e-6
+    assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12
+    v = r["valu"]
+    assert v["peak_tflops"] == 157.3
+    assert abs(v["flops_per_frame"] - (2.5 * N * 10 + N + 25 * 513)) < 1e-9
+    # the two STANDARD halves sum to SURVEY's 5 N log2 N + 5 N + 40 (N/2+1) (~77 kflop)
+    tot = bench.alg_flops_per_frame("analysis", N, False) + bench.alg_flops_per_frame("synthesis", N, False)
+    assert abs(tot - (5 * N * 10 + 5 * N + 40 * 513)) < 1e-9 and 76e3 < tot < 78e3
+    comp = bench.alg_flops_per_frame("compat_analysis", N, True) + bench.alg_flops_per_frame("synthesis", N, True)
+    assert 147e3 < comp < 150e3
+    assert r["bound"] in ("hbm", "valu")
+    # the issue estimate from a static-count file, and `bound` follows the larger fraction
+    isa = tmp_path / "isa.json"
+    isa.write_text(json.dumps({"_sources_sha16": bench.kernel_sources_sha(),
+                               "c3": {"analysis": {"valu_cycles_per_frame": 4000.0}}}))
+    r2 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=str(isa))
+    f = 4000.0 * frames / (1024 * 2e-3 * 2.4e9)
+    assert abs(r2["valu"]["issue_frac_at_peak_clock"] - f) < 1e-12
+    assert r2["bound"] == ("valu" if f > r2["frac"] else "hbm")
+    assert "STALE" not in r2["valu"]["issue_source"]
+    isa.write_text(json.dumps({"_sources_sha16": "0", "c3": {"analysis": {"valu_cycles_per_frame": 1.0}}}))
+    r3 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=str(isa))
+    assert "STALE" in r3["valu"]["issue_source"] and r3["bound"] == "hbm"
+
+
+def test_committed_isa_static_matches_sources():
+    """profiles/isa_static.json must describe this build's kernels (regenerate it with
+    scripts/isa_static.py after a kernel change)."""
+    import json
+    isa = json.load(open(os.path.join(ROOT, "profiles", "isa_static.json")))
+    assert isa["_sources_sha16"] == bench.kernel_sources_sha()
+    for wl, k in (("c3", "analysis"), ("c3", "synthesis"), ("c4", "synthesis"), ("compat", "compat_analysis")):
+        assert isa[wl][k]["valu_cycles_per_frame"] > 0
