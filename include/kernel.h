@@ -4,6 +4,7 @@
 //   CudaPhase::pv_analysis_CUFFT(out2N, fft, in, interm, win, N)   kernel.cu:299-348
 //   CudaPhase::resynthesis_CUFFT(out, back, spec, win, N, hop)     kernel.cu:352-432
 //   CudaPhase::pv_analysis / resynthesis (hand-FFT variants)       kernel.cu:177-218, 262-288
+//   CudaPhase::pv_analysis_RT(out2N, fft, in, interm, [win,] N, &s) kernel.cu:219-260, kernel.h:16
 //   CudaPhase::test_overlap_add(...)                               kernel.cu:289-298
 //   CudaPhase::timer()  PerformanceTimer (karnel/common.h:27-113) on hipEvents
 //
@@ -73,6 +74,34 @@ inline pv_handle* compat_handle(int N, int hop) {
     cache[{N, hop, nf}] = h;
     return h;
 }
+// pv_analysis_RT's handle: REF_COMPAT with the inline periodic Hann of cudaWindow_HanRT
+// (kernel.cu:85-91, = PV_WINDOW_HANN_REF) as its analysis window
+inline pv_handle* rt_handle(int N) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int>, pv_handle*> cache;
+    const int nf = nan_faithful_flag();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({N, nf, dev});
+    if (it != cache.end()) return it->second;
+    pv_config cfg{};
+    cfg.abi_version = PV_ABI_VERSION;
+    cfg.n_samps = N;
+    cfg.hop_div = 2;
+    cfg.effect = PV_TIME_SHIFT;
+    cfg.scale = 1.0f;
+    cfg.mode = PV_MODE_REF_COMPAT;
+    cfg.max_channels = 1;
+    cfg.max_frames = 1;
+    cfg.window = PV_WINDOW_HANN_REF;
+    cfg.nan_faithful = nf;
+    cfg.device = dev;
+    pv_handle* h = nullptr;
+    check(pv_create(&cfg, &h), "pv_create");
+    cache[{N, nf, dev}] = h;
+    return h;
+}
 inline int spec_stride(pv_handle* h) {
     pv_info info{};
     info.abi_version = PV_ABI_VERSION;
@@ -121,6 +150,30 @@ inline void resynthesis(float* output, float* backFrame, float2* frontFrame, flo
                         float* win, int N, int hopSize) {
     (void)intermediary;
     resynthesis_CUFFT(output, backFrame, frontFrame, win, N, hopSize);
+}
+
+// kernel.cu:219-260 (the defined signature; `win` is unused there too): the frame
+// input[0..N) windowed by the inline periodic Hann of cudaWindow_HanRT (kernel.cu:85-91),
+// zero-phase shift + zero pad to 2N (cufftShiftPadZeros), 2N-point forward FFT
+// (computeGPUFFT_RT), then {mag, atanf(Im/Re)} of all 2N bins in place (cudaMagFreq) ->
+// output, all enqueued on *stream (the legacy default stream when stream is null) and not
+// waited for, like the reference.  The FFT is the correct DFT: the reference's hand FFT
+// leaves an odd stage count's result in `fft` (hpfft.cu:169-173), which is
+// not reproduced.  `fft` / `intermediary` are unused (the product stays on chip).
+inline void pv_analysis_RT(float2* output, float2* fft, float* input, float* intermediary, float* win,
+                           int N, hipStream_t* stream) {
+    (void)fft;
+    (void)intermediary;
+    (void)win;
+    pv_handle* h = detail::rt_handle(N);
+    detail::check(pv_analysis(h, input, N, N, 1, 1, (pv_float2*)output, detail::spec_stride(h),
+                              stream ? (void*)*stream : nullptr),
+                  "pv_analysis_RT");
+}
+// kernel.h:16 declares it without `win`
+inline void pv_analysis_RT(float2* output, float2* fft, float* input, float* intermediary, int N,
+                           hipStream_t* stream) {
+    pv_analysis_RT(output, fft, input, intermediary, nullptr, N, stream);
 }
 
 // kernel.cu:289-298: window, shift, unshift, window, overlap-add (identity processing)

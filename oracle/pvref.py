@@ -208,9 +208,12 @@ def compat_process_batch(x, N, hop_div, frames=None, threads=0):
     return out, used
 
 
-def compat_analysis_frame(frame, N, nan_faithful=False):
+def compat_analysis_frame(frame, N, nan_faithful=False, window=None):
+    """kernel.cu:299-348 on one frame; window: float32[N] (None = the Hamming of the
+    4-argument constructor; hann_ref(N) = cudaWindow_HanRT of pv_analysis_RT)."""
     b = np.empty(4 * N, np.float64)
-    lib().pvr_compat_analysis_frame(_c32(frame), N, hamming_ref(N), b, 1 if nan_faithful else 0)
+    w = hamming_ref(N) if window is None else _c32(window)
+    lib().pvr_compat_analysis_frame(_c32(frame), N, w, b, 1 if nan_faithful else 0)
     return b.view(np.complex128)  # (mag + i*phase) per bin, 2N bins
 
 
