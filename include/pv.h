@@ -159,6 +159,10 @@ static inline void pv_unpack_bins(pv_float2 slot0, pv_float2* bin0, pv_float2* b
 }
 
 int pv_abi_version(void);
+/* version of the fp32 PV_STANDARD analysis contract (the exact operation sequence of the
+ * phases and unwrap decisions) this build computes; the CPU oracle states the
+ * version it restates (oracle/pvref.h PVR_CONTRACT_VERSION) and the two must agree */
+int pv_contract_version(void);
 const char* pv_status_string(pv_status s);
 const char* pv_last_error(void); /* thread-local text of the last failure */
 

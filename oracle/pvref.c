@@ -27,6 +27,8 @@ static const float PVR_ATAN_C[10] = {
     0x1.000000p+0f,  -0x1.5554eep-2f, 0x1.9986ecp-3f,  -0x1.23c87ap-3f, 0x1.bd9028p-4f,
     -0x1.506f6cp-4f, 0x1.c2c9f4p-5f,  -0x1.d2ca58p-6f, 0x1.398008p-7f,  -0x1.8ba68ap-10f};
 
+int pvr_contract_version(void) { return PVR_CONTRACT_VERSION; }
+
 /* ------------------------------------------------------------------ tables */
 
 void pvr_hann_periodic(int N, float* w) {
@@ -174,17 +176,25 @@ void pvr_rfft_c32(const float* xw, int N, const pvr_c32* tw, const pvr_c32* tws,
         float orr = 0.5f * (A.y + B.y);
         float oi = 0.5f * (B.x - A.x);
         pvr_c32 w = tws[k];
-        X[k].x = er + fmaf(orr, w.x, -(oi * w.y));
-        X[k].y = ei + fmaf(orr, w.y, oi * w.x);
+        /* contract v2: the odd part's twiddle product accumulated onto the even part with
+         * two fused operations per component (one rounding each), as the GPU's
+         * split_chunk / split_chunk_bp / real_split / bin_l_real */
+        X[k].x = fmaf(orr, w.x, fmaf(-oi, w.y, er));
+        X[k].y = fmaf(orr, w.y, fmaf(oi, w.x, ei));
     }
     X[0].y = 0.0f;
     X[L].y = 0.0f;
 }
 
+/* contract v2: m = -RN_int(d * (1/2pi)) with ONE rounding: fmaf(d, 1/2pi, 1.5 * 2^23) rounds
+ * the exact product onto the integer grid of [2^23, 2^24) (ties to even, as rintf, since the
+ * magic is even); subtracting the magic back is exact (|d| < 3 pi).  The GPU
+ * (pv_device.hpp unwrap_round / unwrap_count) performs the same two operations. */
+#define PVR_RINT_MAGIC 0x1.8p23f
 int pvr_unwrap_count(float phi, float phi_prev, float e) {
     float d = (phi - phi_prev) - e;
-    float q = d * PVR_INV_2PI_F;
-    return -(int)rintf(q);
+    float t = fmaf(d, PVR_INV_2PI_F, PVR_RINT_MAGIC);
+    return -(int)(t - PVR_RINT_MAGIC);
 }
 
 /* ------------------------------------------------------------------ geometry */

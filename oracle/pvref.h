@@ -19,10 +19,14 @@
  *     reference's milestone slides.  Pinned only by this oracle and by
  *     numpy fp64 cross-checks on well-conditioned inputs.
  *
- * Numerical contract (shared, by specification, with the GPU path):
+ * Numerical contract (shared, by specification, with the GPU path; version
+ * PVR_CONTRACT_VERSION, reported by the GPU library as pv_contract_version()):
  *   PV_STANDARD analysis is defined as an exact sequence of IEEE fp32 operations
  *   (radix-2 Stockham FFT of hpfft.cu:145-203 with tabled twiddles, the real-FFT split,
- *   sqrtf, the polynomial atan2 below).  The GPU must reproduce these bit-for-bit, because
+ *   sqrtf, the polynomial atan2 below, the unwrap decision).  Version 2 (round 4): the
+ *   split accumulates the odd part's twiddle product with two fused operations per
+ *   component, and the decision rounds the exact product d * (1/2pi) once (fmaf onto the
+ *   1.5*2^23 integer grid) instead of rounding the product and then rintf.  The GPU must reproduce these bit-for-bit, because
  *   the phase-unwrap decision (round((dphi - e_k)/2pi)) is discontinuous: any ulp of
  *   difference in a noise bin can flip it and change the output phase by 2*pi*rho.
  *   Everything downstream of the integer decisions is well-conditioned and is computed
@@ -36,6 +40,9 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define PVR_CONTRACT_VERSION 2
+int pvr_contract_version(void);
 
 typedef struct { float x, y; } pvr_c32;
 typedef struct { double x, y; } pvr_c64;

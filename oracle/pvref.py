@@ -45,6 +45,7 @@ def lib():
         L.pvr_atan2f.restype = c_float
         L.pvr_fft_c32.argtypes = [_f32p, _f32p, c_int, _f32p, c_int]
         L.pvr_rfft_c32.argtypes = [_f32p, c_int, _f32p, _f32p, _f32p, _f32p]
+        L.pvr_contract_version.restype = c_int
         L.pvr_unwrap_count.argtypes = [c_float, c_float, c_float]
         L.pvr_unwrap_count.restype = c_int
         L.pvr_num_frames.argtypes = [c_long, c_int]
@@ -69,6 +70,11 @@ def lib():
         L.pvr_compat_process_batch.restype = c_int
         _lib = L
     return _lib
+
+
+def contract_version():
+    """version of the fp32 analysis contract this oracle restates (pvref.h)"""
+    return int(lib().pvr_contract_version())
 
 
 def _c32(a):

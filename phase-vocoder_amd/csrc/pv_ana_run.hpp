@@ -24,6 +24,21 @@ constexpr int ana_twl_n() { return ana_tws_min<L>() > 0 ? ana_tws_min<L>() : L; 
 // 2 vs 4: -1 %)
 constexpr int kAnaChunk = 2;
 
+// The per-bin sum of a run's unwrap decisions: at L <= 512 the decision bits unwrap_t summed
+// as uint32 (one v_add_u32 per bin and frame); at L = 1024, whose kernels sit at their
+// 168-VGPR bound and spill with the integer sums (25 VGPRs), the decisions as exact small
+// integers in fp32 (one subtraction more per bin).
+template <int L>
+using ana_acc_t = typename std::conditional<(L <= 512), unsigned, float>::type;
+template <typename Acc>
+__device__ __forceinline__ Acc decision_term(float phi, float phi_prev, float e) {
+    if constexpr (std::is_same<Acc, unsigned>::value) return __float_as_uint(unwrap_t(phi, phi_prev, e));
+    else return unwrap_round(phi, phi_prev, e);
+}
+// S = the sum of the decisions m of the run's frames after its first (n of them)
+__device__ __forceinline__ int decision_sum(unsigned acc, int n) { return (int)((unsigned)n * kRintMagicBits - acc); }
+__device__ __forceinline__ int decision_sum(float acc, int) { return -(int)acc; }
+
 // LDS tables the analysis reads
 struct AnaLds {
     const float2* twl;   // stage-major twiddles, L-point
@@ -42,8 +57,8 @@ constexpr int row_stores() { return PACKED ? E : E + 1; }
 // One wave = one run of frames t0 .. t0 + nfr - 1 of channel c.  The run's first decision
 // m0 = m(t0) needs phi(t0 - 1), the previous run's last frame: it is not recomputed here (no
 // halo frame) but made by k_carry from the two runs' records.  On return phprev = phi of the
-// run's last frame and sacc = -(sum of the decisions of frames t0 + 1 .. t0 + nfr - 1) as
-// exact small integers in fp32.  Rows go out with non-temporal stores (they are read back by
+// run's last frame and sacc = the sum over frames t0 + 1 .. t0 + nfr - 1 of the decision
+// terms (ana_acc_t).  Rows go out with non-temporal stores (they are read back by
 // another launch, long after they would have left the caches).  rec (nullable): the run
 // record {S, phi(t0), phi(t0 + nfr - 1)} (kRecFields rows of bins_pad words, phases as their
 // float bits).
@@ -51,7 +66,7 @@ template <int L, bool EKL, int D, bool PACKED>
 __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
                                         float e_lane, int* rec, float (&phprev)[Geo<L>::E + 1],
-                                        float (&sacc)[Geo<L>::E + 1]) {
+                                        ana_acc_t<L> (&sacc)[Geo<L>::E + 1]) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
@@ -68,7 +83,8 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     const float e_L = EKL ? lds_ld(&ekl[L]) : __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(e_lane)));
     const float* xc = p.x + (long long)c * p.ldx;
     float2* specc = p.spec + (long long)c * p.ld_spec;
-    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = 0.0f; })
+    using Acc = ana_acc_t<L>;
+    PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = Acc(0); })
 
     // One frame: window + FFT + split + atan2, spectrum row, decisions, from raw samples.
     auto window = [&](const float2 (&xr)[E], float2 (&z)[E]) {
@@ -94,10 +110,10 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         // decision is against phprev = 0, not phi(t0 - 1): it is taken back out of S at once
         // (wave-uniform branch, once per run) and the phase goes to the record instead.
         {
-            const float mr = unwrap_round(phL, phprev[E], e_L);
-            sacc[E] += mr;
+            const Acc mb = decision_term<Acc>(phL, phprev[E], e_L);
+            sacc[E] += mb;
             if (u == 0) {
-                sacc[E] -= mr;
+                sacc[E] -= mb;
                 if (rec != nullptr && lane == 0) rec[BP + L] = __float_as_int(phL);
             }
         }
@@ -138,11 +154,11 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                         // bin L: the same value and address on every lane
                         __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
                     }
-                    // m = -mr (frame t0: as bin L above)
-                    const float mr = unwrap_round(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
-                    sacc[i] += mr;
+                    // decision bits (frame t0: as bin L above)
+                    const Acc mb = decision_term<Acc>(ph, phprev[i], EKL ? lds_ld(&ekl[k]) : e_lane);
+                    sacc[i] += mb;
                     if (u == 0) {
-                        sacc[i] -= mr;
+                        sacc[i] -= mb;
                         if (rec != nullptr) rec[BP + k] = __float_as_int(ph);
                     }
                 }
@@ -226,7 +242,8 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         window(xr, z);
         frame(u, z);
     }
-    if (rec != nullptr) PV_FOR_BINS(E, lane, { rec[k] = -(int)sacc[i]; rec[2 * BP + k] = __float_as_int(phprev[i]); })
+    if (rec != nullptr)
+        PV_FOR_BINS(E, lane, { rec[k] = decision_sum(sacc[i], nfr - 1); rec[2 * BP + k] = __float_as_int(phprev[i]); })
 }
 
 }  // namespace pv

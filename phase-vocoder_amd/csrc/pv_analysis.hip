@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L
     // run record {S, phi(t0), phi(last)}: phi(t0) is stored as soon as it is known, the rest
     // after the loop
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad : nullptr;
-    float phprev[E + 1], sacc[E + 1];
+    float phprev[E + 1];
+    ana_acc_t<L> sacc[E + 1];
     ana_run<L, EKL, D, PACKED>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c, t0, nfr,
                                e_lane, rec, phprev, sacc);
 }

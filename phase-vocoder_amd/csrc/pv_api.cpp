@@ -408,6 +408,9 @@ extern "C" {
 
 int pv_abi_version(void) { return PV_ABI_VERSION; }
 
+// 2 (round 4): fused real-split accumulation, one-rounding unwrap decision (pv_device.hpp)
+int pv_contract_version(void) { return 2; }
+
 const char* pv_status_string(pv_status s) {
     switch (s) {
         case PV_OK: return "PV_OK";

@@ -174,6 +174,26 @@ __device__ __forceinline__ void vm_wait(f2v (&xr)[E]) {
     for (int q = 0; q < E; ++q) asm volatile("" : "+v"(xr[q]));  // uses stay after the wait
 }
 
+// Lane 0 only: (bx, by) <- (ax, ay) by two v_mov_b32 under exec & 1 (the lane-0 partner fix-up
+// of the real-FFT splits, whose partner bins are lane 0's own registers).  A v_mov issues at
+// the full VALU rate, a v_cndmask_b32 select at half (profiles/r04_valu_probe3.jsonl: 2.25 vs
+// 4.15 cycles per wave-instruction); exec is restored, and lane 0 is only written if active.
+__device__ __forceinline__ void lane0_mov2(float& bx, float& by, float ax, float ay) {
+#ifndef PV_LANE0_SELECT  // (A/B build: the select form)
+    unsigned long long saved;
+    asm("s_mov_b64 %2, exec\n\t"
+        "s_and_b64 exec, exec, 1\n\t"
+        "v_mov_b32 %0, %3\n\t"
+        "v_mov_b32 %1, %4\n\t"
+        "s_mov_b64 exec, %2"
+        : "+v"(bx), "+v"(by), "=&s"(saved) : "v"(ax), "v"(ay) : "scc");  // s_and_b64 writes SCC
+#else
+    const bool l0 = __lane_id() == 0;
+    bx = l0 ? ax : bx;
+    by = l0 ? ay : by;
+#endif
+}
+
 __device__ __forceinline__ float2 cmul(float2 b, float2 w) {
     float2 t;
     t.x = __builtin_fmaf(b.x, w.x, -(b.y * w.y));
@@ -320,16 +340,23 @@ __device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
     *cs = __builtin_amdgcn_cosf(rev);
 }
 
-// unwrap decision of the contract (oracle pvr_unwrap_count)
+// unwrap decision of the contract (oracle pvr_unwrap_count, contract v2): the exact product
+// d * (1/2pi) rounded once onto the integer grid of [2^23, 2^24) by an fma with the magic
+// 1.5 * 2^23 (ties to even, as rint: the magic is even); t - magic is then exact.  Two fast
+// VALU operations instead of a multiply and a (quarter-rate) v_rndne.
+constexpr float kRintMagic = 0x1.8p23f;
+constexpr unsigned kRintMagicBits = 0x4B400000u;
+// t = magic + rint(d / 2pi): the decision's bits (m = -(bits(t) - kRintMagicBits))
+__device__ __forceinline__ float unwrap_t(float phi, float phi_prev, float e) {
+    const float d = (phi - phi_prev) - e;
+    return __builtin_fmaf(d, kInv2Pi, kRintMagic);
+}
 // rint of the scaled deviation as a float: m = -unwrap_round(...) (exact small integer)
 __device__ __forceinline__ float unwrap_round(float phi, float phi_prev, float e) {
-    float d = (phi - phi_prev) - e;
-    return __builtin_rintf(d * kInv2Pi);
+    return unwrap_t(phi, phi_prev, e) - kRintMagic;
 }
 __device__ __forceinline__ int unwrap_count(float phi, float phi_prev, float e) {
-    float d = (phi - phi_prev) - e;
-    float q = d * kInv2Pi;
-    return -(int)__builtin_rintf(q);
+    return -(int)(__float_as_uint(unwrap_t(phi, phi_prev, e)) - kRintMagicBits);
 }
 
 // ------------------------------------------------------------------ wave-local LDS sync

@@ -19,8 +19,8 @@ __device__ __forceinline__ float2 real_split(const float2* tile, const float2* _
     const float orr = 0.5f * (A.y + Bz.y);
     const float oi = 0.5f * (Bz.x - A.x);
     const float2 tw = tws[k];
-    float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
-    float Xi = ei + __builtin_fmaf(orr, tw.y, oi * tw.x);
+    float Xr = __builtin_fmaf(orr, tw.x, __builtin_fmaf(-oi, tw.y, er));  // contract v2
+    float Xi = __builtin_fmaf(orr, tw.y, __builtin_fmaf(oi, tw.x, ei));
     if (k == 0 || k == L) Xi = 0.0f;
     return make_float2(Xr, Xi);
 }
@@ -63,8 +63,8 @@ __device__ __forceinline__ void split_chunk(const float2* tile, const float2* tw
         const float ei = h * (A[c].y - Bz[c].y);
         const float orr = h * (A[c].y + Bz[c].y);
         const float oi = h * (Bz[c].x - A[c].x);
-        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
-        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
+        float Xr = __builtin_fmaf(orr, tw[c].x, __builtin_fmaf(-oi, tw[c].y, er));  // contract v2
+        float Xi = __builtin_fmaf(orr, tw[c].y, __builtin_fmaf(oi, tw[c].x, ei));
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
         X[c] = make_float2(Xr, Xi);
     }
@@ -89,7 +89,7 @@ constexpr int bin_at(int pos) { return !PACKED ? pos : pos == 0 ? 0 : pos == 1 ?
 // A = Z[k], k = l + 64 i, is the lane's own register and B = Z[(L - k) mod L] =
 // Z[(64 - l) + 64 (E - 1 - i)] is register slot E-1-i of lane 64 - l — a lane reversal by
 // ds_bpermute (crossbar only).  Lane 0's partners are its own registers (Z[(L - 64 i) mod L]
-// = slot (E - i) mod E): it selects them before the permute and reads from itself.  Same
+// = slot (E - i) mod E): its permute reads itself and lane0_mov2 then puts them in.  Same
 // operands, same operations as split_chunk: bit-identical bins.  Chunk positions P0 ..
 // P0 + CH - 1 are bins bin_at<E, PACKED>(position) (positions past E are dummies).
 template <int L, int CH, bool TWICE, int P0, bool PACKED = false>
@@ -97,7 +97,6 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
                                                float2 (&X)[CH]) {
     constexpr int E = Geo<L>::E;
     const int rev = ((64 - lane) & 63) << 2;
-    const bool l0 = lane == 0;
     const float2* baseT = twsl + lane;
     float2 A[CH], Bz[CH], tw[CH];
     static_for<0, CH>([&](auto cc) {
@@ -107,9 +106,18 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
             A[c] = v[slot_reg<L>(i)];
             const float2 o = v[slot_reg<L>(E - 1 - i)];
             const float2 m = v[slot_reg<L>((E - i) & (E - 1))];
-            const float sx = l0 ? m.x : o.x, sy = l0 ? m.y : o.y;
-            Bz[c].x = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sx)));
-            Bz[c].y = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sy)));
+            if constexpr (L >= 1024) {
+                // (the L = 1024 kernels sit at their 168-VGPR bound: m is selected before the
+                // permute rather than kept live across it, which spills there)
+                const bool l0 = lane == 0;
+                const float sx = l0 ? m.x : o.x, sy = l0 ? m.y : o.y;
+                Bz[c].x = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sx)));
+                Bz[c].y = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(sy)));
+            } else {
+                Bz[c].x = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(o.x)));
+                Bz[c].y = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(o.y)));
+                lane0_mov2(Bz[c].x, Bz[c].y, m.x, m.y);  // lane 0 read itself: its partner is m
+            }
             tw[c] = lds_ld(&baseT[64 * i]);
         } else {
             // bin L, computed by every lane (all store the same value to one address):
@@ -129,8 +137,8 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
         const float ei = h * (A[c].y - Bz[c].y);
         const float orr = h * (A[c].y + Bz[c].y);
         const float oi = h * (Bz[c].x - A[c].x);
-        float Xr = er + __builtin_fmaf(orr, tw[c].x, -(oi * tw[c].y));
-        float Xi = ei + __builtin_fmaf(orr, tw[c].y, oi * tw[c].x);
+        float Xr = __builtin_fmaf(orr, tw[c].x, __builtin_fmaf(-oi, tw[c].y, er));  // contract v2
+        float Xi = __builtin_fmaf(orr, tw[c].y, __builtin_fmaf(oi, tw[c].x, ei));
         if (i >= E || (i == 0 && lane == 0)) Xi = 0.0f;  // bins 0 and L are real
         X[c] = make_float2(Xr, Xi);
     });
@@ -154,7 +162,7 @@ __device__ __forceinline__ void bin_l_real(const float2 (&v)[Geo<L>::E], const f
     const float er = h * (ax + ax);
     const float orr = h * (ay + ay);
     const float oi = h * (ax - ax);
-    const float Xr = er + __builtin_fmaf(orr, tw.x, -(oi * tw.y));
+    const float Xr = __builtin_fmaf(orr, tw.x, __builtin_fmaf(-oi, tw.y, er));  // contract v2
     const float zero = 0.0f;
     const float m = __builtin_amdgcn_sqrtf(__builtin_fmaf(Xr, Xr, zero * zero));
     magL = TWICE ? 0.5f * m : m;
@@ -265,8 +273,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             const float tqf = (float)tq;
             PV_FOR_BINS(E, lane, {
                 // m = -rint(dev); R <- fract(R - m p/q) = fract(R + rint(dev) p/q)
-                const float d = (ph[i] - phprev[i]) - ekv[i];
-                const float mr = __builtin_rintf(d * kInv2Pi);
+                const float mr = unwrap_round(ph[i], phprev[i], ekv[i]);
                 float R = __int_as_float(M[i]);
                 if (add_decision) R = __builtin_amdgcn_fractf(__builtin_fmaf(mr, npq, R));
                 M[i] = __float_as_int(R);
@@ -424,7 +431,8 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
 #pragma unroll
     for (int q = 0; q < E; ++q) {
         const float2 A = Yr[q];
-        const float2 Bc = (lane == 0) ? Yr[E - q] : Bp[q];
+        float2 Bc = Bp[q];
+        lane0_mov2(Bc.x, Bc.y, Yr[E - q].x, Yr[E - q].y);  // lane 0: its own register E - q
         float2 tw;  // e^{-2 pi i k/N}, k = lane + 64 q
         if constexpr (TwS::ON) tw = twr.v[q];
         else tw = lds_ld(&twsl[lane + 64 * q]);

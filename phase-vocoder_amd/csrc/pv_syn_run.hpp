@@ -350,8 +350,10 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     };
 
     // the self-tracked prefetch needs registers that are never spilled or copied while the
-    // loads are in flight: only at L <= 512, where the kernels fit without spills
-    constexpr bool FASTOK = ROLA && L <= 512;
+    // loads are in flight: only at L = 512, where the kernels fit without spills and no
+    // register copy sits between a row load and its vmcnt (scripts/prefetch_hazards.py,
+    // tests/test_abi.py; at L <= 256 the compiler copies the row buffers)
+    constexpr bool FASTOK = ROLA && L == 512;
     const bool fast = FASTOK && nfr == p.F && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
     if (FASTOK && fast) {
         // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]

@@ -79,7 +79,8 @@ def cost_of(op, text, extra):
     return SLOW
 
 
-def frame_loop(asm, prefix):
+def loops_of(asm, prefix):
+    """every loop body (backward branch) of the function, as (start, end, instructions)"""
     labels, insts = {}, []
     for line in function_body(asm, prefix):
         m = re.match(r"^(\.LBB\w+):", line)
@@ -90,17 +91,42 @@ def frame_loop(asm, prefix):
         if not s or s.startswith((";", ".")):
             continue
         insts.append((s.split()[0], s))
-    best = None
+    out = []
     for i, (op, s) in enumerate(insts):
         if op.startswith("s_cbranch") or op == "s_branch":
             tgt = s.split()[-1]
             if tgt in labels and labels[tgt] <= i:
-                seg = insts[labels[tgt]:i + 1]
-                ops = [o for o, _ in seg]
-                has_perm = any(o.startswith("ds_bpermute") for o in ops)
-                has_store = any(o.startswith("global_store") for o in ops)
-                if has_perm and has_store and (best is None or len(seg) < len(best)):
-                    best = seg
+                out.append((labels[tgt], i, insts[labels[tgt]:i + 1]))
+    return out
+
+
+def price(seg, extra):
+    cnt, cyc = Counter(), 0.0
+    for op, text in seg:
+        if op.startswith("v_"):
+            c = cost_of(op, text, extra)
+            cyc += c
+            cnt["valu_trans" if c == TRANS else "valu_packed" if op.startswith("v_pk_") else "valu"] += 1
+        elif op.startswith("ds_"):
+            cnt["lds"] += 1
+        elif op.startswith(("global_", "buffer_")):
+            cnt["vmem"] += 1
+    return cnt, cyc
+
+
+def frame_loop(asm, prefix, trans_pf, extra):
+    """The steady-state frame loop: among the innermost loops that hold a frame's work (LDS
+    permutes and global stores), the one with the fewest VALU cycles per frame (the path every
+    full run takes; the bounds-checked variants for the channel ends cost more)."""
+    cands = [(a, b, seg) for a, b, seg in loops_of(asm, prefix)
+             if any(o.startswith("ds_bpermute") for o, _ in seg) and any(o.startswith("global_store") for o, _ in seg)]
+    inner = [c for c in cands if not any(o is not c and c[0] <= o[0] and o[1] <= c[1] for o in cands)]
+    best = None
+    for a, b, seg in inner:
+        cnt, cyc = price(seg, extra)
+        fpl = max(1, round(cnt["valu_trans"] / trans_pf))
+        if best is None or cyc / fpl < best[2] / best[1]:
+            best = (seg, fpl, cyc, cnt)
     return best
 
 
@@ -123,21 +149,10 @@ def main():
                 subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *fl, "-o", asm, os.path.join(CSRC, src)],
                                check=True, stderr=subprocess.DEVNULL)
                 cache[(src, tuple(fl))] = asm
-            seg = frame_loop(asm, prefix)
-            if seg is None:
+            best = frame_loop(asm, prefix, trans_pf, extra)
+            if best is None:
                 continue
-            cnt = Counter()
-            cyc = 0.0
-            for op, text in seg:
-                if op.startswith("v_"):
-                    c = cost_of(op, text, extra)
-                    cyc += c
-                    cnt["valu_trans" if c == TRANS else "valu_packed" if op.startswith("v_pk_") else "valu"] += 1
-                elif op.startswith("ds_"):
-                    cnt["lds"] += 1
-                elif op.startswith(("global_", "buffer_")):
-                    cnt["vmem"] += 1
-            fpl = max(1, round(cnt["valu_trans"] / trans_pf))  # frames per loop trip
+            seg, fpl, cyc, cnt = best
             out.setdefault(wl, {})[key] = {"symbol": prefix, "loop_instructions": len(seg),
                                            "frames_per_trip": fpl,
                                            "counts_per_trip": dict(cnt),

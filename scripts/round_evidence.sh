@@ -23,7 +23,7 @@ STEPS="${STEPS:-tests c3 c2 c4 compat rt prof pmc}"
 for s in $STEPS; do
   case $s in
     probe3) run valu_probe3 300 scripts/valu_probe3 ;;
-    tests) run pytest_gpu 700 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread; tail -3 gpurun_out/pytest_gpu.log ;;
+    tests) run pytest_gpu 700 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}; tail -3 gpurun_out/pytest_gpu.log ;;
     c3) run bench_c3 400 python bench.py ;;
     c3q) run bench_c3 300 python bench.py --no-cpu ;;
     c2) run bench_c2 300 python bench.py --workload c2 ;;

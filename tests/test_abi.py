@@ -6,6 +6,7 @@ import subprocess
 
 import pytest
 
+from conftest import ROOT
 from pvamd import _lib
 
 
@@ -33,6 +34,14 @@ def test_abi_version_and_status_strings():
     assert L.pv_abi_version() == _lib.ABI_VERSION == 4
     assert L.pv_status_string(0) == b"PV_OK"
     assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
+
+
+def test_contract_version_matches_oracle():
+    """The GPU's fp32 analysis contract and the oracle's restatement are versioned together
+    (DESIGN.md §3.2): a library and an oracle of different versions would disagree in the
+    last bits of the phases and hence in unwrap decisions."""
+    import pvref
+    assert _lib.lib().pv_contract_version() == pvref.contract_version() == 2
 
 
 def test_frame_count_is_main_cpp_loop():
@@ -159,3 +168,27 @@ def test_fused_stamps_diagnostic_compiles():
             cmd[1:1] = ["-x", "hip"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_device_asm_has_no_prefetch_or_scc_hazards(tmp_path):
+    """The self-tracked prefetch loads (inline asm, invisible to the compiler's waits) must not
+    have their registers read, written or copied before the vmcnt that retires them, and no
+    inline asm that writes SCC may sit between an SCC writer and its reader
+    (scripts/prefetch_hazards.py; both once produced wrong results and a GPU fault)."""
+    import subprocess
+    import sys
+    csrc = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
+    flags = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+             "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S"]
+    procs, outs = [], []
+    for src in ("pv_analysis", "pv_kernels", "pv_fused", "pv_rt"):
+        out = str(tmp_path / f"{src}.s")
+        extra = ["-fno-slp-vectorize"] if src == "pv_analysis" else []
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *flags, *extra, "-I", os.path.join(ROOT, "include"),
+                                       "-o", out, os.path.join(csrc, f"{src}.hip")],
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        outs.append(out)
+    assert all(p.wait(timeout=600) == 0 for p in procs)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "prefetch_hazards.py"), *outs],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("0 hazard(s)"), r.stdout[-3000:]
