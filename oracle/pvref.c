@@ -162,13 +162,134 @@ void pvr_fft_c32(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* tw, int inve
     if (in != data) memcpy(data, in, sizeof(pvr_c32) * (size_t)L);
 }
 
+/* ---- contract v3 FFT (L = N/2 in [128, 512], E = L/64 points per GPU lane) ----
+ * A Stockham FFT of twiddle-first radix-R passes: pass P has span S = E^P and radix
+ * R = min(E, L/S); for every j < L/R (m = j mod S) the R points a_q = in[j + q L/R] are
+ * multiplied by the table twiddles T_P[m][q] = e^{-2 pi i m q/(R S)} (q >= 1; none in pass 0,
+ * where m = 0), transformed by the R-point DIF below (compile-time internal twiddles: 1, -i,
+ * W8 = e^{-i pi/4}, W8^3) and written to out[(j/S) R S + m + S k] (register f of the GPU
+ * holds y_k for k = bitrev(f), DIF order).  Exactly the operations of pv_device.hpp
+ * fft_pass_v3. */
+#define PVR_W8C 0x1.6a09e6p-1f /* (float)(1/sqrt 2) */
+
+static inline int ilog2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
+static inline int bitrevi(int v, int bits) {
+    int r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((v >> i) & 1) << (bits - 1 - i);
+    return r;
+}
+
+int pvr_fft_v3_applies(int L) { return L >= 128 && L <= 512; }
+
+int pvr_fft_v3_table_size(int L) {
+    const int E = L / 64;
+    int n = 0;
+    for (int S = E; S < L; S *= (E < L / S ? E : L / S)) n += S * ((E < L / S ? E : L / S) - 1);
+    return n;
+}
+
+void pvr_fft_v3_table(int L, pvr_c32* t) {
+    const int E = L / 64;
+    int off = 0;
+    for (int S = E; S < L;) {
+        const int R = E < L / S ? E : L / S;
+        for (int m = 0; m < S; ++m)
+            for (int q = 1; q < R; ++q) {
+                /* e^{-2 pi i m q/(R S)} = the L-point master entry (m q L/(R S)) mod L */
+                const long idx = ((long)m * q * (L / (R * S))) % L;
+                const double a = 2.0 * PVR_PI_D * (double)idx / (double)L;
+                t[off + m * (R - 1) + (q - 1)].x = (float)cos(a);
+                t[off + m * (R - 1) + (q - 1)].y = (float)(-sin(a));
+            }
+        off += S * (R - 1);
+        S *= R;
+    }
+}
+
+/* the R-point DIF of contract v3 on t[0..R-1] (R in {2, 4, 8}) */
+static void dif_v3(pvr_c32* t, int R, int inverse) {
+    const float c = PVR_W8C;
+    for (int h = R / 2; h >= 1; h /= 2)
+        for (int b = 0; b < R; b += 2 * h)
+            for (int i = 0; i < h; ++i) {
+                const pvr_c32 u = t[b + i], v = t[b + i + h];
+                pvr_c32 d;
+                if (i > 0 && 2 * i == h) {        /* -i (forward) / +i (inverse) rotation */
+                    if (!inverse) { d.x = u.y - v.y; d.y = v.x - u.x; }
+                    else { d.x = v.y - u.y; d.y = u.x - v.x; }
+                } else {
+                    const pvr_c32 e = {u.x - v.x, u.y - v.y};
+                    if (i == 0) {
+                        d = e;
+                    } else {
+                        pvr_c32 s;
+                        if (4 * i == h) {         /* W8^1 = (c, -c); inverse (c, c) */
+                            if (!inverse) { s.x = e.x + e.y; s.y = e.y - e.x; }
+                            else { s.x = e.x - e.y; s.y = e.x + e.y; }
+                        } else {                  /* 4i == 3h: W8^3 = (-c, -c); inverse (-c, c) */
+                            if (!inverse) { s.x = e.y - e.x; s.y = -e.x - e.y; }
+                            else { s.x = -e.x - e.y; s.y = e.x - e.y; }
+                        }
+                        d.x = s.x * c;
+                        d.y = s.y * c;
+                    }
+                }
+                t[b + i].x = u.x + v.x;
+                t[b + i].y = u.y + v.y;
+                t[b + i + h] = d;
+            }
+}
+
+void pvr_fft_c32_v3(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* ptab, int inverse) {
+    const int E = L / 64;
+    pvr_c32* in = data;
+    pvr_c32* out = tmp;
+    int off = 0;
+    for (int S = 1, P = 0; S < L; ++P) {
+        const int R = E < L / S ? E : L / S;
+        const int r = ilog2i(R);
+        for (int j = 0; j < L / R; ++j) {
+            const int m = j % S;
+            pvr_c32 t[8];
+            for (int q = 0; q < R; ++q) t[q] = in[j + q * (L / R)];
+            if (P > 0)
+                for (int q = 1; q < R; ++q) {
+                    pvr_c32 tw = ptab[off + m * (R - 1) + (q - 1)];
+                    if (inverse) tw.y = -tw.y;
+                    t[q] = cmul_c(t[q], tw);
+                }
+            dif_v3(t, R, inverse);
+            for (int f = 0; f < R; ++f) out[(j / S) * R * S + m + S * bitrevi(f, r)] = t[f];
+        }
+        if (P > 0) off += S * (R - 1);
+        pvr_c32* sw = in; in = out; out = sw;
+        S *= R;
+    }
+    if (in != data) memcpy(data, in, sizeof(pvr_c32) * (size_t)L);
+}
+
+/* the contract's real FFT of N raw samples x with the analysis window w: x * w rounded, then
+ * pvr_rfft_c32 */
+void pvr_rfft_win_c32(const float* x, const float* w, int N, const pvr_c32* tw, const pvr_c32* tws,
+                      pvr_c32* X, pvr_c32* work) {
+    float* xw = (float*)malloc(sizeof(float) * N);
+    for (int i = 0; i < N; ++i) xw[i] = x[i] * w[i];
+    pvr_rfft_c32(xw, N, tw, tws, X, work);
+    free(xw);
+}
+
 void pvr_rfft_c32(const float* xw, int N, const pvr_c32* tw, const pvr_c32* tws,
                   pvr_c32* X, pvr_c32* work) {
     const int L = N / 2;
     pvr_c32* z = work;
     pvr_c32* tmp = work + L;
     for (int n = 0; n < L; ++n) { z[n].x = xw[2 * n]; z[n].y = xw[2 * n + 1]; }
-    pvr_fft_c32(z, tmp, L, tw, 0);
+    if (pvr_fft_v3_applies(L)) pvr_fft_c32_v3(z, tmp, L, tw, 0);
+    else pvr_fft_c32(z, tmp, L, tw, 0);
+    pvr_split_c32(z, L, tws, X);
+}
+
+void pvr_split_c32(const pvr_c32* z, int L, const pvr_c32* tws, pvr_c32* X) {
     for (int k = 0; k <= L; ++k) {
         pvr_c32 A = z[k % L], B = z[(L - k) % L];
         float er = 0.5f * (A.x + B.x);
@@ -279,12 +400,14 @@ static void std_ana_init(std_ana_ctx* c, int N, int hop) {
     c->N = N; c->L = N / 2; c->B = N / 2 + 1; c->hop = hop;
     c->w = (float*)malloc(sizeof(float) * N);
     c->xw = (float*)malloc(sizeof(float) * N);
-    c->tw = (pvr_c32*)malloc(sizeof(pvr_c32) * (N / 4 + 1));
+    c->tw = (pvr_c32*)malloc(sizeof(pvr_c32) * (N / 2 + 1));
     c->tws = (pvr_c32*)malloc(sizeof(pvr_c32) * c->B);
     c->work = (pvr_c32*)malloc(sizeof(pvr_c32) * N);
     c->X = (pvr_c32*)malloc(sizeof(pvr_c32) * c->B);
     pvr_hann_periodic(N, c->w);
-    pvr_fft_twiddles(c->L, c->tw);
+    /* the FFT's table: contract v3 pass table (L <= 512) or the radix-2 master table */
+    if (pvr_fft_v3_applies(c->L)) pvr_fft_v3_table(c->L, c->tw);
+    else pvr_fft_twiddles(c->L, c->tw);
     pvr_split_twiddles(N, c->tws);
 }
 
@@ -297,10 +420,10 @@ static void std_ana_frame(std_ana_ctx* c, const float* x, long n, long start, fl
                           float* phase) {
     for (int i = 0; i < c->N; ++i) {
         long idx = start + i;
-        float v = (idx < n) ? x[idx] : 0.0f; /* defined deviation: OOB samples read as 0 */
-        c->xw[i] = v * c->w[i];
+        c->xw[i] = (idx < n) ? x[idx] : 0.0f; /* defined deviation: OOB samples read as 0 */
     }
-    pvr_rfft_c32(c->xw, c->N, c->tw, c->tws, c->X, c->work);
+    /* the raw frame: the window is applied inside (contract v3: folded into the FFT) */
+    pvr_rfft_win_c32(c->xw, c->w, c->N, c->tw, c->tws, c->X, c->work);
     for (int k = 0; k < c->B; ++k) {
         float re = c->X[k].x, im = c->X[k].y;
         mag[k] = sqrtf(fmaf(re, re, im * im));

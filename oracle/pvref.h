@@ -26,7 +26,10 @@
  *   sqrtf, the polynomial atan2 below, the unwrap decision).  Version 2 (round 4): the
  *   split accumulates the odd part's twiddle product with two fused operations per
  *   component, and the decision rounds the exact product d * (1/2pi) once (fmaf onto the
- *   1.5*2^23 integer grid) instead of rounding the product and then rintf.  The GPU must reproduce these bit-for-bit, because
+ *   1.5*2^23 integer grid) instead of rounding the product and then rintf.  Version 3:
+ *   for L = N/2 in [128, 512] the FFT is a Stockham FFT of twiddle-first radix-(L/64) passes
+ *   with R-point DIF butterflies (pvr_fft_c32_v3); L >= 1024 keeps the radix-2 Stockham
+ *   stages.  The GPU must reproduce these bit-for-bit, because
  *   the phase-unwrap decision (round((dphi - e_k)/2pi)) is discontinuous: any ulp of
  *   difference in a noise bin can flip it and change the output phase by 2*pi*rho.
  *   Everything downstream of the integer decisions is well-conditioned and is computed
@@ -41,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PVR_CONTRACT_VERSION 2
+#define PVR_CONTRACT_VERSION 3
 int pvr_contract_version(void);
 
 typedef struct { float x, y; } pvr_c32;
@@ -62,6 +65,14 @@ float pvr_atan2f(float y, float x);
 /* radix-2 Stockham (hpfft.cu:145-167 stage structure); result in data; tmp = L scratch */
 void pvr_fft_c32(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* tw, int inverse);
 /* real FFT of N windowed samples -> N/2+1 bins (contract of the GPU analysis) */
+/* contract v3 FFT (L in [128, 512]; see pvref.c) */
+int pvr_fft_v3_applies(int L);
+int pvr_fft_v3_table_size(int L);
+void pvr_fft_v3_table(int L, pvr_c32* t);
+void pvr_fft_c32_v3(pvr_c32* data, pvr_c32* tmp, int L, const pvr_c32* ptab, int inverse);
+void pvr_split_c32(const pvr_c32* z, int L, const pvr_c32* tws, pvr_c32* X);
+void pvr_rfft_win_c32(const float* x, const float* w, int N, const pvr_c32* tw, const pvr_c32* tws,
+                      pvr_c32* X, pvr_c32* work);
 void pvr_rfft_c32(const float* xw, int N, const pvr_c32* tw, const pvr_c32* tws,
                   pvr_c32* X, pvr_c32* work);
 int pvr_unwrap_count(float phi, float phi_prev, float e);

@@ -45,6 +45,13 @@ def lib():
         L.pvr_atan2f.restype = c_float
         L.pvr_fft_c32.argtypes = [_f32p, _f32p, c_int, _f32p, c_int]
         L.pvr_rfft_c32.argtypes = [_f32p, c_int, _f32p, _f32p, _f32p, _f32p]
+        L.pvr_fft_v3_applies.argtypes = [c_int]
+        L.pvr_fft_v3_applies.restype = c_int
+        L.pvr_fft_v3_table_size.argtypes = [c_int]
+        L.pvr_fft_v3_table_size.restype = c_int
+        L.pvr_fft_v3_table.argtypes = [c_int, _f32p]
+        L.pvr_fft_c32_v3.argtypes = [_f32p, _f32p, c_int, _f32p, c_int]
+        L.pvr_rfft_win_c32.argtypes = [_f32p, _f32p, c_int, _f32p, _f32p, _f32p, _f32p]
         L.pvr_contract_version.restype = c_int
         L.pvr_unwrap_count.argtypes = [c_float, c_float, c_float]
         L.pvr_unwrap_count.restype = c_int
@@ -135,12 +142,51 @@ def fft_c32(z, inverse=False):
     return buf.view(np.complex64)
 
 
+def fft_v3_applies(L):
+    return bool(lib().pvr_fft_v3_applies(int(L)))
+
+
+def fft_v3_table(L):
+    """contract v3 pass table (pvref.c pvr_fft_v3_table): float32 pairs"""
+    t = np.empty(2 * max(1, lib().pvr_fft_v3_table_size(L)), np.float32)
+    lib().pvr_fft_v3_table(L, t)
+    return t
+
+
+def analysis_fft_table(L):
+    """the table the contract's analysis FFT of L points uses"""
+    return fft_v3_table(L) if fft_v3_applies(L) else fft_twiddles(L)
+
+
+def fft_c32_v3(z, inverse=False):
+    """Contract v3 FFT (L in [128, 512], pvref.c pvr_fft_c32_v3)."""
+    z = np.ascontiguousarray(z, dtype=np.complex64)
+    L = z.shape[0]
+    assert fft_v3_applies(L)
+    buf = z.view(np.float32).copy()
+    tmp = np.empty_like(buf)
+    lib().pvr_fft_c32_v3(buf, tmp, L, fft_v3_table(L), 1 if inverse else 0)
+    return buf.view(np.complex64)
+
+
 def rfft_c32(xw):
+    """the contract's real FFT of windowed samples (v3 FFT for N/2 <= 512, no window fold)"""
     xw = _c32(xw)
     N = xw.shape[0]
     X = np.empty(2 * (N // 2 + 1), np.float32)
     work = np.empty(2 * N, np.float32)
-    lib().pvr_rfft_c32(xw, N, fft_twiddles(N // 2), split_twiddles(N), X, work)
+    lib().pvr_rfft_c32(xw, N, analysis_fft_table(N // 2), split_twiddles(N), X, work)
+    return X.view(np.complex64)
+
+
+def rfft_win_c32(x, w):
+    """the contract's analysis transform of raw samples x with window w (x * w, then
+    rfft_c32)"""
+    x, w = _c32(x), _c32(w)
+    N = x.shape[0]
+    X = np.empty(2 * (N // 2 + 1), np.float32)
+    work = np.empty(2 * N, np.float32)
+    lib().pvr_rfft_win_c32(x, w, N, analysis_fft_table(N // 2), split_twiddles(N), X, work)
     return X.view(np.complex64)
 
 

@@ -81,6 +81,27 @@ void stage_twiddles(int L, std::vector<float2>& t) {
         for (int idx = 0; idx < Ns; ++idx) t[Ns - 1 + idx] = tw_entry((long long)idx * (L / (2 * Ns)), L);
 }
 
+// The FFT table of an L-point transform: the contract-v3 pass table for L in [128, 512]
+// (pass P >= 1: S rows of R - 1 entries e^{-2 pi i m q/(R S)}, the oracle's
+// pvr_fft_v3_table), the stage-major radix-2 table otherwise; L entries either way.
+void fft_table(int L, std::vector<float2>& t) {
+    if (L < 128 || L > 512) {
+        stage_twiddles(L, t);
+        return;
+    }
+    t.assign(L, make_float2(0.f, 0.f));
+    const int E = L / 64;
+    int off = 0;
+    for (int S = E; S < L;) {
+        const int R = std::min(E, L / S);
+        for (int m = 0; m < S; ++m)
+            for (int q = 1; q < R; ++q)
+                t[off + m * (R - 1) + (q - 1)] = tw_entry(((long long)m * q * (L / (R * S))) % L, L);
+        off += S * (R - 1);
+        S *= R;
+    }
+}
+
 void split_twiddles(int N, std::vector<float2>& t) {
     t.resize(N / 2 + 1);
     for (int k = 0; k <= N / 2; ++k) t[k] = tw_entry(k, N);
@@ -408,8 +429,9 @@ extern "C" {
 
 int pv_abi_version(void) { return PV_ABI_VERSION; }
 
-// 2 (round 4): fused real-split accumulation, one-rounding unwrap decision (pv_device.hpp)
-int pv_contract_version(void) { return 2; }
+// 2 (round 4): fused real-split accumulation, one-rounding unwrap decision (pv_device.hpp);
+// 3: twiddle-first radix-E FFT passes with the window folded in, L <= 512 (fft_pass v3)
+int pv_contract_version(void) { return 3; }
 
 const char* pv_status_string(pv_status s) {
     switch (s) {
@@ -602,11 +624,11 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
 
     // ---- twiddles
     std::vector<float2> t;
-    stage_twiddles(h->L_ana, t);
+    fft_table(h->L_ana, t);
     if ((st = upload(&h->d_tw_ana, t)) != PV_OK) return bail(st);
     split_twiddles(2 * h->L_ana, t);
     if ((st = upload(&h->d_tws_ana, t)) != PV_OK) return bail(st);
-    stage_twiddles(h->L_syn, t);
+    fft_table(h->L_syn, t);
     if ((st = upload(&h->d_tw_syn, t)) != PV_OK) return bail(st);
     split_twiddles(N, t);
     if ((st = upload(&h->d_tws_syn, t)) != PV_OK) return bail(st);
@@ -1190,7 +1212,7 @@ extern "C" pv_status pv_fft_c2c(const pv_float2* in, pv_float2* out, int n, int 
         auto it = g_fft_tw.find({dev, n});
         if (it == g_fft_tw.end()) {
             std::vector<float2> t;
-            stage_twiddles(n, t);
+            fft_table(n, t);
             pv_status st = upload(&tw, t);
             if (st != PV_OK) return st;
             g_fft_tw[{dev, n}] = tw;

@@ -600,11 +600,129 @@ __device__ __forceinline__ void load_tw0(float2 (&tw0)[Geo<L>::E], const float2*
 // STORE_LAST the result is left in `tile` in natural order (padded indexing); without it
 // the last pass's output stays in v, where register v[g*R + f] holds point
 // lane + 64 g + S_last * bitrev_r(f)  (= lane + 64 c, see last_slot()).
+// ------------------------------------------------------------------ FFT contract v3
+// For L in [128, 512] (E = L/64 <= 8) a pass is one twiddle-first radix-R Stockham step per
+// group (oracle pvr_fft_c32_v3): the R points a_q (q >= 1) are multiplied by the pass-table
+// twiddles T_P[m][q] = e^{-+2 pi i m q/(R S)}, m = j mod S (none in pass 0), then an R-point
+// DIF whose internal twiddles are compile-time: 1, -i (a swapped, negated difference: the
+// op_sel / neg modifiers of one v_pk_add), W8 and W8^3 (a swizzled v_pk_add and a v_pk_mul by
+// 1/sqrt 2).  Register f ends up holding y_{bitrev(f)}: the same output layout as the radix-2
+// stages (pass_store / last_slot unchanged).  Per L = 512 transform: 112 packed operations
+// instead of 128 (radix-2 stages: a table twiddle per butterfly).  (Folding the analysis
+// window into pass 0's first stage saves 4 more but holds the window pairs in 9 more VGPRs:
+// the analysis drops to 4 waves/SIMD, measured slower.)  L >= 1024 keeps the radix-2 stages:
+// its last pass would need an S (R - 1) ~ L-entry table, which costs the analysis a workgroup
+// per CU of LDS.
+template <int L>
+constexpr bool fft_v3() { return L >= 128 && L <= 512; }
+// pass table offset of pass P >= 1: sum over 1 <= P' < P of S_P' (R_P' - 1)
+template <int L>
+constexpr int v3_off(int P) {
+    int off = 0;
+    for (int p = 1; p < P; ++p) {
+        const int S = 1 << (p * Geo<L>::RLOG);
+        const int R = 1 << cmin(Geo<L>::RLOG, Geo<L>::LOG2L - p * Geo<L>::RLOG);
+        off += S * (R - 1);
+    }
+    return off;
+}
+constexpr float kW8c = 0x1.6a09e6p-1f;  // (float)(1/sqrt 2), oracle PVR_W8C
+
+// (u - v) * (-i) (forward) or * (+i) (inverse): one v_pk_add, each half a single rounding
+template <bool INV>
+__device__ __forceinline__ f2v pk_rot_sub(f2v u, f2v v) {
+    f2v d;
+    if constexpr (!INV)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(d) : "v"(u), "v"(v));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(u), "v"(v));
+    return d;
+}
+// e * W8 (W8 = e^{-i pi/4}; conj when INV) or e * W8^3: the swizzled sum s of the oracle's
+// dif_v3, then s * (1/sqrt 2)
+template <bool W83, bool INV>
+__device__ __forceinline__ f2v pk_w8(f2v e) {
+    f2v sw, d;
+    if constexpr (!W83 && !INV)  // (e.x + e.y, e.y - e.x)
+        asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(sw) : "v"(e));
+    else if constexpr (!W83 && INV)  // (e.x - e.y, e.x + e.y)
+        asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[0,1]" : "=v"(sw) : "v"(e));
+    else if constexpr (W83 && !INV)  // (e.y - e.x, -e.x - e.y)
+        asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(sw) : "v"(e));
+    else  // (-e.x - e.y, e.x - e.y)
+        asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(sw) : "v"(e));
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(sw), "s"(f2v{kW8c, kW8c}));
+    return d;
+}
+
+// The R-point DIF of contract v3 on t[0..R-1] (oracle dif_v3)
+template <int R, bool INV>
+__device__ __forceinline__ void dif_v3(f2v* t) {
+    static_assert(R == 2 || R == 4 || R == 8, "contract v3 radices");
+    static_for<0, ilog2c(R)>([&](auto sc) {
+        constexpr int st = decltype(sc)::value;
+        constexpr int h = R >> (st + 1);
+        static_for<0, R / 2>([&](auto bc) {
+            constexpr int bi = decltype(bc)::value;
+            constexpr int b = (bi / h) * 2 * h, i = bi % h;
+            const f2v u = t[b + i], v = t[b + i + h];
+            f2v d;
+            if constexpr (i > 0 && 2 * i == h) {
+                d = pk_rot_sub<INV>(u, v);
+            } else {
+                const f2v e = u - v;
+                if constexpr (i == 0) d = e;
+                else d = pk_w8<(4 * i == 3 * h), INV>(e);
+            }
+            t[b + i] = u + v;
+            t[b + i + h] = d;
+        });
+    });
+}
+
+template <int L, int P, bool INV>
+__device__ __forceinline__ void fft_pass_v3(float2 (&v)[Geo<L>::E], const float2* tw, int lane) {
+    using G_ = Geo<L>;
+    constexpr int S = 1 << (P * G_::RLOG);
+    constexpr int r = cmin(G_::RLOG, G_::LOG2L - P * G_::RLOG);
+    constexpr int R = 1 << r;
+    constexpr int NG = G_::E / R;
+    constexpr int E = G_::E;
+    f2v a[E];
+#pragma unroll
+    for (int q = 0; q < E; ++q) a[q] = f2v{v[q].x, v[q].y};
+    if constexpr (P > 0) {
+        // the pass's (R - 1) NG table twiddles as one batch of LDS reads (volatile: not paired)
+        float2 w[NG][R - 1];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int m = (lane + 64 * g) & (S - 1);
+            const float2* row = tw + v3_off<L>(P) + m * (R - 1);
+#pragma unroll
+            for (int q = 1; q < R; ++q) w[g][q - 1] = lds_ld(&row[q - 1]);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int q = 1; q < R; ++q) a[g * R + q] = cmul_v<INV>(a[g * R + q], f2v{w[g][q - 1].x, w[g][q - 1].y});
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) dif_v3<R, INV>(&a[g * R]);
+#pragma unroll
+    for (int q = 0; q < E; ++q) v[q] = make_float2(a[q].x, a[q].y);
+}
+
 template <int L, bool INV, bool STORE_LAST = true, int P = 0, int TWS_MIN = 0>
 __device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, const float2* tw,
                                         const float2 (&tw0)[Geo<L>::E], int lane,
                                         const float2* tws = nullptr) {
-    fft_pass<L, P, INV, TWS_MIN>(v, tw, tw0, lane, tws);
+    if constexpr (fft_v3<L>()) {
+        (void)tw0;
+        (void)tws;
+        fft_pass_v3<L, P, INV>(v, tw, lane);
+    } else {
+        fft_pass<L, P, INV, TWS_MIN>(v, tw, tw0, lane, tws);
+    }
     if constexpr (P + 1 < Geo<L>::NPASS) {
         pass_store<L, P>(v, tile, lane);
         wave_lds_sync();

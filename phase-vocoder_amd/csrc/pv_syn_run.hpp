@@ -300,7 +300,9 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     // the pre-step's split twiddles of the lane's bins in registers for the run: L = 1024
     // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy) and the L = 512
     // per-lane kernels (within their 3 waves/SIMD budget)
-    using TwS = typename std::conditional<((L == 1024 || (L == 512 && LANEK)) && ROLA), TwReg<E>, NoTwReg>::type;
+    // (not the L = 512 pitch kernel with out hop 128: with the contract-v3 FFT it would spill)
+    using TwS = typename std::conditional<((L == 1024 || (L == 512 && LANEK && !(MODE == 2 && DT == 1))) && ROLA),
+                                          TwReg<E>, NoTwReg>::type;
     TwS twr;
     if constexpr (TwS::ON) {
 #pragma unroll

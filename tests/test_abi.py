@@ -41,7 +41,7 @@ def test_contract_version_matches_oracle():
     (DESIGN.md §3.2): a library and an oracle of different versions would disagree in the
     last bits of the phases and hence in unwrap decisions."""
     import pvref
-    assert _lib.lib().pv_contract_version() == pvref.contract_version() == 2
+    assert _lib.lib().pv_contract_version() == pvref.contract_version() == 3
 
 
 def test_frame_count_is_main_cpp_loop():
