@@ -94,18 +94,19 @@ float pvr_atan2f(float y, float x) {
      * y), without a special case */
     if (mx < 0x1p-126f) mx = 0x1p-126f;
     /* a = mn / mx without a division: reciprocal of mx from an integer seed (relative
-     * error <= 5.1e-2) and three Newton steps e = 1 - mx r, r += r e (fmaf), then one
-     * product; <= 6e-8 relative for normal mx (audio spectra are far from the fp32
-     * range ends).  The GPU (pv_device.hpp atan2_pv) performs the same operations. */
+     * error <= 5.1e-2), a cubic and a Newton step (below), then one product; <= 6e-8
+     * relative for normal mx (audio spectra are far from the fp32 range ends).  The GPU
+     * (pv_device.hpp atan2_pv / atan2_pv2) performs the same operations. */
     uint32_t mb;
     memcpy(&mb, &mx, sizeof mb);
     mb = 0x7EF311C3u - mb;
     float r0;
     memcpy(&r0, &mb, sizeof r0);
+    /* contract v3: one cubic step r (1 + e + e^2) (|e| <= 5.1e-2 -> 1.3e-4) and one Newton
+     * step (-> ~2e-8): five fmaf instead of the three Newton steps' six */
     float e = fmaf(-mx, r0, 1.0f);
-    r0 = fmaf(r0, e, r0);
-    e = fmaf(-mx, r0, 1.0f);
-    r0 = fmaf(r0, e, r0);
+    float e2 = fmaf(e, e, e);
+    r0 = fmaf(r0, e2, r0);
     e = fmaf(-mx, r0, 1.0f);
     r0 = fmaf(r0, e, r0);
     float a = mn * r0;

@@ -214,12 +214,11 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(mx) : "v"(x), "v"(y), "s"(0x1p-126f));
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
     // a = mn / mx by the contract's division-free reciprocal (oracle pvr_atan2f): integer
-    // seed + three fmaf Newton steps + one product (8 VALU, no v_rcp / div_scale chain)
+    // seed + a cubic and a Newton fmaf step + one product (7 VALU, no v_rcp / div_scale chain)
     float r = __uint_as_float(0x7EF311C3u - __float_as_uint(mx));
-    float e = __builtin_fmaf(-mx, r, 1.0f);
-    r = __builtin_fmaf(r, e, r);
-    e = __builtin_fmaf(-mx, r, 1.0f);
-    r = __builtin_fmaf(r, e, r);
+    float e = __builtin_fmaf(-mx, r, 1.0f);  // contract v3: a cubic step, then a Newton step
+    const float e2 = __builtin_fmaf(e, e, e);
+    r = __builtin_fmaf(r, e2, r);
     e = __builtin_fmaf(-mx, r, 1.0f);
     r = __builtin_fmaf(r, e, r);
     float a = mn * r;
@@ -256,10 +255,9 @@ __device__ __forceinline__ f2v atan2_pv2(float y0, float x0, float y1, float x1)
     mn = f2v{u0, u1};
     r = f2v{__uint_as_float(0x7EF311C3u - __float_as_uint(t0)), __uint_as_float(0x7EF311C3u - __float_as_uint(t1))};
     const f2v one = f2v{1.0f, 1.0f};
-    f2v e = __builtin_elementwise_fma(-mx, r, one);
-    r = __builtin_elementwise_fma(r, e, r);
-    e = __builtin_elementwise_fma(-mx, r, one);
-    r = __builtin_elementwise_fma(r, e, r);
+    f2v e = __builtin_elementwise_fma(-mx, r, one);  // contract v3: cubic step + Newton step
+    const f2v e2 = __builtin_elementwise_fma(e, e, e);
+    r = __builtin_elementwise_fma(r, e2, r);
     e = __builtin_elementwise_fma(-mx, r, one);
     r = __builtin_elementwise_fma(r, e, r);
     const f2v a = mn * r;
@@ -301,10 +299,9 @@ __device__ __forceinline__ f2v atan_ratio_pv2(float y0, float x0, float y1, floa
     mn = f2v{u0, u1};
     r = f2v{__uint_as_float(0x7EF311C3u - __float_as_uint(t0)), __uint_as_float(0x7EF311C3u - __float_as_uint(t1))};
     const f2v one = f2v{1.0f, 1.0f};
-    f2v e = __builtin_elementwise_fma(-mx, r, one);
-    r = __builtin_elementwise_fma(r, e, r);
-    e = __builtin_elementwise_fma(-mx, r, one);
-    r = __builtin_elementwise_fma(r, e, r);
+    f2v e = __builtin_elementwise_fma(-mx, r, one);  // contract v3: cubic step + Newton step
+    const f2v e2 = __builtin_elementwise_fma(e, e, e);
+    r = __builtin_elementwise_fma(r, e2, r);
     e = __builtin_elementwise_fma(-mx, r, one);
     r = __builtin_elementwise_fma(r, e, r);
     const f2v a = mn * r;

@@ -106,7 +106,11 @@ __device__ __forceinline__ void split_chunk_bp(const float2 (&v)[Geo<L>::E], con
             A[c] = v[slot_reg<L>(i)];
             const float2 o = v[slot_reg<L>(E - 1 - i)];
             const float2 m = v[slot_reg<L>((E - i) & (E - 1))];
+#ifdef PV_LANE0_PRESEL
+            if constexpr (true) {
+#else
             if constexpr (L >= 1024) {
+#endif
                 // (the L = 1024 kernels sit at their 168-VGPR bound: m is selected before the
                 // permute rather than kept live across it, which spills there)
                 const bool l0 = lane == 0;
@@ -349,7 +353,11 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                     constexpr int i0 = decltype(ig)::value * G;
                     i2v sc[G];
                     float2 f[G];
-                    if constexpr (L >= 1024) {
+        #ifdef PV_LANE0_PRESEL
+            if constexpr (true) {
+#else
+            if constexpr (L >= 1024) {
+#endif
 #pragma unroll
                         for (int j = 0; j < G; ++j) sc[j] = scn[j];
                     } else {
@@ -423,7 +431,12 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     float2 Bp[E];
 #pragma unroll
     for (int q = 0; q < E; ++q) {
+#ifdef PV_LANE0_PRESEL
+        // lane 0 sends (and reads back) its own register E - q
+        const float2 o = (lane == 0) ? Yr[E - q] : Yr[E - 1 - q];
+#else
         const float2 o = Yr[E - 1 - q];
+#endif
         Bp[q].x = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.x)));
         Bp[q].y = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.y)));
     }
@@ -432,7 +445,9 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     for (int q = 0; q < E; ++q) {
         const float2 A = Yr[q];
         float2 Bc = Bp[q];
+#ifndef PV_LANE0_PRESEL
         lane0_mov2(Bc.x, Bc.y, Yr[E - q].x, Yr[E - q].y);  // lane 0: its own register E - q
+#endif
         float2 tw;  // e^{-2 pi i k/N}, k = lane + 64 q
         if constexpr (TwS::ON) tw = twr.v[q];
         else tw = lds_ld(&twsl[lane + 64 * q]);

@@ -76,7 +76,8 @@ def lib():
     L = ctypes.CDLL(os.path.abspath(LIB_PATH))
     vp, ll, i, f = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
     L.pv_abi_version.restype = i
-    L.pv_contract_version.restype = i
+    if hasattr(L, "pv_contract_version"):  # (A/B builds of older revisions lack it)
+        L.pv_contract_version.restype = i
     L.pv_status_string.argtypes = [i]
     L.pv_status_string.restype = ctypes.c_char_p
     L.pv_last_error.restype = ctypes.c_char_p
