@@ -431,12 +431,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     float2 Bp[E];
 #pragma unroll
     for (int q = 0; q < E; ++q) {
-#ifdef PV_LANE0_PRESEL
-        // lane 0 sends (and reads back) its own register E - q
-        const float2 o = (lane == 0) ? Yr[E - q] : Yr[E - 1 - q];
-#else
         const float2 o = Yr[E - 1 - q];
-#endif
         Bp[q].x = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.x)));
         Bp[q].y = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.y)));
     }
@@ -444,10 +439,10 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
 #pragma unroll
     for (int q = 0; q < E; ++q) {
         const float2 A = Yr[q];
-        float2 Bc = Bp[q];
-#ifndef PV_LANE0_PRESEL
-        lane0_mov2(Bc.x, Bc.y, Yr[E - q].x, Yr[E - q].y);  // lane 0: its own register E - q
-#endif
+        // lane 0: its own register E - q.  (A select, not lane0_mov2: here the exec-masked
+        // moves measured ~1 % slower, profiles/r04_ab_lane0.txt — they must wait for the
+        // permute before the moves, the select can sit at the use.)
+        const float2 Bc = (lane == 0) ? Yr[E - q] : Bp[q];
         float2 tw;  // e^{-2 pi i k/N}, k = lane + 64 q
         if constexpr (TwS::ON) tw = twr.v[q];
         else tw = lds_ld(&twsl[lane + 64 * q]);

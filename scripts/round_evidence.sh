@@ -34,6 +34,12 @@ for s in $STEPS; do
     prof_c4) prof prof_c4 400 --workload c4 --steps 40 --warmup 3 --no-cpu ;;
     prof_compat) prof prof_compat 400 --workload compat --steps 20 --warmup 3 --no-cpu ;;
     prof_c2) prof prof_c2 400 --workload c2 --no-cpu ;;
+    traffic_c3|traffic_c4)
+      w=${s#traffic_}; rm -rf gpurun_out/pmc
+      args="--calib"; [ $w = c4 ] && args="--calib --N 2048 --effect p --scale 1.5"
+      PMC_SETS=scripts/pmc_sets_traffic.txt PROF_ARGS="$args" timeout -k 10 400 bash scripts/pmc_session.sh > gpurun_out/pmc_$w.log 2>&1
+      rc=$?; tail -3 gpurun_out/pmc_$w.log; [ $rc -ne 0 ] && exit $rc
+      rm -rf gpurun_out/pmc_$w && mv gpurun_out/pmc gpurun_out/pmc_$w ;;
     pmc)
       rm -rf gpurun_out/pmc
       PMC_SETS=scripts/pmc_sets_r1.txt PROF_ARGS="--calib" timeout -k 10 900 bash scripts/pmc_session.sh > gpurun_out/pmc_session.log 2>&1

@@ -54,7 +54,17 @@ for k, cs in per.items():
     res[name if name not in res else k] = {"kernel": k, "read_bytes_per_launch": rd,
                                            "write_bytes_per_launch": wr,
                                            "bytes_per_launch": rd + wr}
-res["_workload"] = os.environ.get("PV_TRAFFIC_WORKLOAD", "c3")  # what prof_kernels.py ran
 res["_layout"] = os.environ.get("PV_TRAFFIC_LAYOUT", "packed")   # its spectrum row layout
-json.dump(res, open(out, "w"), indent=1)
-print(json.dumps(res, indent=1))
+wl = os.environ.get("PV_TRAFFIC_WORKLOAD", "c3")                  # what prof_kernels.py ran
+# profiles/traffic.json holds one entry per workload: {"c3": {...}, "c4": {...}}
+allw = {}
+if os.path.exists(out):
+    try:
+        allw = json.load(open(out))
+        if "_workload" in allw:  # the single-workload form of earlier rounds
+            allw = {allw["_workload"]: allw}
+    except ValueError:
+        allw = {}
+allw[wl] = res
+json.dump(allw, open(out, "w"), indent=1)
+print(json.dumps({wl: res}, indent=1))

@@ -33,6 +33,27 @@ def test_bench_two_ranks_on_one_gpu(cuda):
     assert abs(d["value"] * d["ms_per_step"] * d["steps"] * 1e-3 - frames) <= 1e-6 * frames
 
 
+@pytest.mark.gpu
+def test_bench_two_ranks_config4(cuda):
+    """The 8-GPU configuration itself (BASELINE.json configs[3]: N=2048, hop 512, pitch 1.5,
+    the L = 1024 table blob) through launch_ranks + broadcast_tables + the max-reductions."""
+    env = dict(os.environ, PV_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "c4",
+                        "--channels", "8", "--seconds", "1", "--steps", "3", "--warmup", "1", "--no-cpu"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["N"] == 2048 and d["config"]["hop"] == 512
+    assert d["tables_broadcast"]["bit_identical_to_local"] is True
+    assert d["tables_broadcast"]["bytes"] > 0
+    chk = d["rms_vs_oracle"]
+    assert chk["pass"] and chk["ranks"] == 2 and chk["all_finite"]
+
+
 def test_bench_rejects_gpus_world_size_mismatch():
     env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
