@@ -266,7 +266,10 @@ pv_status pv_test_overlap_add(const float* in, const float* win, const float* ba
 
 /* Per-kernel timing with hipEvents recorded on the launch stream (for bench.py).  enable:
  * 0 off, 1 every launch, k > 1 the launches of every k-th pv_analysis / pv_resynthesis /
- * pv_process call (an event record costs the queue a few us). */
+ * pv_process / pv_rt_push call (an event record costs the queue a few us).  Within one call
+ * the launches share events: launch i+1's timing starts at launch i's stop event, so any
+ * GPU idle time while the host enqueues launch i+1 counts toward launch i+1 (a bias of a few
+ * us at most, visible only on the short carry / seam launches). */
 pv_status pv_profile_enable(pv_handle* h, int enable);
 /* names[i] (static strings), total ms and launch count of each kernel since the last
  * reset; returns number of kernels written (<= cap). Synchronises the recorded events. */

@@ -83,9 +83,10 @@ void stage_twiddles(int L, std::vector<float2>& t) {
 
 // The FFT table of an L-point transform: the contract-v3 pass table for L in [128, 512]
 // (pass P >= 1: S rows of R - 1 entries e^{-2 pi i m q/(R S)}, the oracle's
-// pvr_fft_v3_table), the stage-major radix-2 table otherwise; L entries either way.
-void fft_table(int L, std::vector<float2>& t) {
-    if (L < 128 || L > 512) {
+// pvr_fft_v3_table), the stage-major radix-2 table otherwise; L entries either way.  v3: the
+// pass table at any L (the batched synthesis's L = 1024 inverse FFT, which no contract binds).
+void fft_table(int L, std::vector<float2>& t, bool v3 = false) {
+    if (!v3 && (L < 128 || L > 512)) {
         stage_twiddles(L, t);
         return;
     }
@@ -101,6 +102,11 @@ void fft_table(int L, std::vector<float2>& t) {
         S *= R;
     }
 }
+
+// d_tw_syn: the synthesis-side L-point table (stage-major or v3, fft_table), then at L = 1024
+// the v3 pass table of the batched synthesis's inverse FFT (k_synthesis reads tw + L; the
+// real-time and fused kernels run the analysis transform from the first table too)
+int tw_syn_len(int L) { return L == 1024 ? 2 * L : L; }
 
 void split_twiddles(int N, std::vector<float2>& t) {
     t.resize(N / 2 + 1);
@@ -174,7 +180,7 @@ struct DeviceGuard {
     }
 };
 
-// one public call (pv_analysis / pv_resynthesis / pv_process): with a stride k > 1 only every
+// one public call (pv_analysis / pv_resynthesis / pv_process / pv_rt_push): with a stride k > 1 only every
 // k-th call's launches get events (each event record costs the queue a few us, which a
 // 40-us single-stream step would otherwise carry in its timed region)
 void prof_tick(pv_handle* h) {
@@ -341,7 +347,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.q = h->q;
     p.q_pow2 = h->q_pow2;
     p.inv_q = h->inv_q;
-    p.tw = h->d_tw_syn;
+    p.tw = h->d_tw_syn + (tw_syn_len(h->L_syn) - h->L_syn);  // L = 1024: the v3 pass table
     p.tws = h->d_tws_syn;
     p.gain = h->d_gain;
     p.rot = (h->mode == PV_MODE_REF_COMPAT) ? h->N / 2 : 0;
@@ -629,6 +635,11 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     split_twiddles(2 * h->L_ana, t);
     if ((st = upload(&h->d_tws_ana, t)) != PV_OK) return bail(st);
     fft_table(h->L_syn, t);
+    if (tw_syn_len(h->L_syn) > h->L_syn) {
+        std::vector<float2> t3;
+        fft_table(h->L_syn, t3, true);
+        t.insert(t.end(), t3.begin(), t3.end());
+    }
     if ((st = upload(&h->d_tw_syn, t)) != PV_OK) return bail(st);
     split_twiddles(N, t);
     if ((st = upload(&h->d_tws_syn, t)) != PV_OK) return bail(st);
@@ -800,7 +811,7 @@ std::vector<TableSeg> table_segments(const pv_handle* h) {
             {h->d_gain, sizeof(float) * N},
             {h->d_tw_ana, sizeof(float2) * h->L_ana},
             {h->d_tws_ana, sizeof(float2) * (h->L_ana + 1)},
-            {h->d_tw_syn, sizeof(float2) * h->L_syn},
+            {h->d_tw_syn, sizeof(float2) * tw_syn_len(h->L_syn)},
             {h->d_tws_syn, sizeof(float2) * (N / 2 + 1)},
             {h->d_ek, sizeof(float) * B},
             {h->d_jk_mod, sizeof(unsigned) * B},
@@ -1101,6 +1112,7 @@ pv_status pv_rt_push(pv_rt* rt, const float* in, long long ldi, int nframes, flo
     p.q_pow2 = h->q_pow2;
     p.inv_q = h->inv_q;
     hipStream_t s = (hipStream_t)stream;
+    prof_tick(h);  // one public call: the profile stride counts pv_rt_push calls too
     PV_LAUNCH(h, KRT, s, pv::launch_rt(h->L_syn, h->pitch ? 2 : 0, p, s));
     return PV_OK;
 }

@@ -610,8 +610,10 @@ __device__ __forceinline__ void load_tw0(float2 (&tw0)[Geo<L>::E], const float2*
 // the analysis drops to 4 waves/SIMD, measured slower.)  L >= 1024 keeps the radix-2 stages:
 // its last pass would need an S (R - 1) ~ L-entry table, which costs the analysis a workgroup
 // per CU of LDS.
-template <int L>
-constexpr bool fft_v3() { return L >= 128 && L <= 512; }
+// X: also at L = 1024 (radices 16, 16, 4; the batched synthesis's inverse transform, which no
+// contract binds — its table is pv_api.cpp's second d_tw_syn block)
+template <int L, bool X = false>
+constexpr bool fft_v3() { return (L >= 128 && L <= 512) || (X && L == 1024); }
 // pass table offset of pass P >= 1: sum over 1 <= P' < P of S_P' (R_P' - 1)
 template <int L>
 constexpr int v3_off(int P) {
@@ -653,9 +655,19 @@ __device__ __forceinline__ f2v pk_w8(f2v e) {
 }
 
 // The R-point DIF of contract v3 on t[0..R-1] (oracle dif_v3)
+// e * W16^i, i odd (R = 16 only, outside the contract: W16^{1,3,5,7} = c - i s, s - i c,
+// -s - i c, -c - i s with c = cos(pi/8), s = sin(pi/8)); conj when INV
+template <int I, bool INV>
+__device__ __forceinline__ f2v w16_odd(f2v e) {
+    constexpr float c = 0x1.d906bcp-1f, sn = 0x1.87de2ap-2f;
+    constexpr float wr = (I == 1) ? c : (I == 3) ? sn : (I == 5) ? -sn : -c;
+    constexpr float wi = (I == 1) ? -sn : (I == 3) ? -c : (I == 5) ? -c : -sn;
+    return cmul_v<INV, true>(e, f2v{wr, wi});
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void dif_v3(f2v* t) {
-    static_assert(R == 2 || R == 4 || R == 8, "contract v3 radices");
+    static_assert(R == 2 || R == 4 || R == 8 || R == 16, "v3 radices");
     static_for<0, ilog2c(R)>([&](auto sc) {
         constexpr int st = decltype(sc)::value;
         constexpr int h = R >> (st + 1);
@@ -669,6 +681,7 @@ __device__ __forceinline__ void dif_v3(f2v* t) {
             } else {
                 const f2v e = u - v;
                 if constexpr (i == 0) d = e;
+                else if constexpr (h == 8 && (i & 1)) d = w16_odd<i, INV>(e);
                 else d = pk_w8<(4 * i == 3 * h), INV>(e);
             }
             t[b + i] = u + v;
@@ -709,11 +722,11 @@ __device__ __forceinline__ void fft_pass_v3(float2 (&v)[Geo<L>::E], const float2
     for (int q = 0; q < E; ++q) v[q] = make_float2(a[q].x, a[q].y);
 }
 
-template <int L, bool INV, bool STORE_LAST = true, int P = 0, int TWS_MIN = 0>
+template <int L, bool INV, bool STORE_LAST = true, int P = 0, int TWS_MIN = 0, bool V3X = false>
 __device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, const float2* tw,
                                         const float2 (&tw0)[Geo<L>::E], int lane,
                                         const float2* tws = nullptr) {
-    if constexpr (fft_v3<L>()) {
+    if constexpr (fft_v3<L, V3X>()) {
         (void)tw0;
         (void)tws;
         fft_pass_v3<L, P, INV>(v, tw, lane);
@@ -725,7 +738,7 @@ __device__ __forceinline__ void fft_run(float2 (&v)[Geo<L>::E], float2* tile, co
         wave_lds_sync();
         pass_load<L, P + 1>(v, tile, lane);
         wave_lds_sync();
-        fft_run<L, INV, STORE_LAST, P + 1, TWS_MIN>(v, tile, tw, tw0, lane, tws);
+        fft_run<L, INV, STORE_LAST, P + 1, TWS_MIN, V3X>(v, tile, tw, tw0, lane, tws);
     } else if constexpr (STORE_LAST) {
         pass_store<L, P>(v, tile, lane);
         wave_lds_sync();

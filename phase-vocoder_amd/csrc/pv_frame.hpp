@@ -204,7 +204,8 @@ struct SynLds {
 };
 
 // One synthesis frame from the spectrum row sv (mag, phase of the lane's bins k = lane +
-// 64 i, i < E, and k = L on lane 0).  MODE 0/2 STANDARD stretch/pitch (unwrap state M,
+// 64 i, i < E, and k = L on lane 0).  MODE 0/2 STANDARD stretch/pitch (MODE 3: pitch with
+// at most one source per bin — ratio >= 1 — fixed at compile time) (unwrap state M,
 // phprev updated; add_decision = false for a run's first frame, whose decision the carry
 // already holds), MODE 1 REF_COMPAT (kernel.cu:121-129 y-bug).  tq = (t + 1) mod q.
 // Result: STORE_LAST: time samples in tile (natural order, padded); else the inverse
@@ -238,7 +239,7 @@ struct TwReg {
 // unwrap state is neither read nor updated; phc = fma(rho / 2 pi, phi, +0) is bit for bit
 // what the RACC path computes with q = 1 (R = tj = +0).
 template <int L, int MODE, bool STORE_LAST, bool QPOW2 = false, bool KREG = false, bool RACC = false,
-          bool Q1 = false, typename Hook = NoHook, typename TwS = NoTwReg>
+          bool Q1 = false, typename Hook = NoHook, typename TwS = NoTwReg, bool V3X = false>
 __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], bool add_decision,
                                             unsigned tq, int (&M)[Geo<L>::E + 1],
                                             float (&phprev)[Geo<L>::E + 1], const PhaseMap& pm,
@@ -315,8 +316,60 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             })
         }
         }  // !RACC
-        if constexpr (MODE == 2) {
+        // (PV_ABL_*: diagnostic ablations for A/B timing only — wrong results)
+#ifdef PV_ABL_NOGATHER
+        if constexpr (false) {
+#else
+        if constexpr (MODE == 2 || MODE == 3) {
+#endif
             float2 Y[E + 1];
+            if constexpr (MODE == 3) {
+            // at most one source per bin (pitch ratio >= 1): srcl holds each bin's source as a
+            // byte offset into the tile, slot L + 1 (a zero written here every frame) when no
+            // source maps there.  Every lane gathers every bin, bin L included (lanes != 0
+            // read bin L's source too and ignore it: no exec-masked blocks), and no selects:
+            // 4-byte map reads, one tile read and the sin/cos per bin.
+            PV_FOR_BINS(E, lane, { if (i < E) tile[k] = make_float2(mag[i], phc[i]); })
+            {
+                // bin L from lane 0, the zero slot from the others (one store, no branch)
+                const bool l0 = lane == 0;
+                tile[l0 ? L : L + 1] = make_float2(l0 ? mag[E] : 0.0f, l0 ? phc[E] : 0.0f);
+            }
+            wave_lds_sync();
+            const unsigned* srco = reinterpret_cast<const unsigned*>(srcl);
+            const char* tb = reinterpret_cast<const char*>(tile);
+            constexpr int G = (L >= 1024) ? 4 : 1;
+            constexpr int NGRP = (E + G) / G;
+            auto offs_reads = [&](auto ig, unsigned (&o)[G]) {
+                static_for<0, G>([&](auto jj) {
+                    constexpr int i = decltype(ig)::value * G + decltype(jj)::value;
+                    if constexpr (i <= E) o[decltype(jj)::value] = lds_ld(&srco[(i == E) ? L : lane + 64 * i]);
+                });
+            };
+            unsigned on[G];
+            offs_reads(std::integral_constant<int, 0>{}, on);
+            static_for<0, NGRP>([&](auto ig) {
+                constexpr int i0 = decltype(ig)::value * G;
+                unsigned o[G];
+                float2 f[G];
+#pragma unroll
+                for (int j = 0; j < G; ++j) o[j] = on[j];
+                static_for<0, G>([&](auto jj) {
+                    constexpr int j = decltype(jj)::value;
+                    if constexpr (i0 + j <= E) f[j] = lds_ld(reinterpret_cast<const float2*>(tb + o[j]));
+                });
+                if constexpr (decltype(ig)::value + 1 < NGRP)
+                    offs_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, on);
+                static_for<0, G>([&](auto jj) {
+                    constexpr int j = decltype(jj)::value;
+                    if constexpr (i0 + j <= E) {
+                        float sn, cs;
+                        sincos_rev(f[j].y, &sn, &cs);
+                        Y[i0 + j] = make_float2(f[j].x * cs, f[j].x * sn);
+                    }
+                });
+            });
+            } else {
             PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
             wave_lds_sync();
             // {first source, count} in one 8-byte read; the first source's {mag, phase}
@@ -396,6 +449,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
             } else {
                 gather(std::false_type{});
             }
+            }  // MODE 2
             wave_lds_sync();
             PV_FOR_BINS(E, lane, {
                 float2 y = Y[i];
@@ -435,7 +489,7 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         Bp[q].x = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.x)));
         Bp[q].y = __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane, __float_as_int(o.y)));
     }
-    wave_lds_sync();  // the FFT's first tile store stays after the reads above (MODE 2)
+    wave_lds_sync();  // the FFT's first tile store stays after the reads above (MODE 2, 3)
 #pragma unroll
     for (int q = 0; q < E; ++q) {
         const float2 A = Yr[q];
@@ -461,7 +515,9 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         z[q] = make_float2(Z.x, Z.y);
     }
     wave_lds_sync();
-    fft_run<L, true, STORE_LAST>(z, tile, twl, tw0, lane);
+#ifndef PV_ABL_NOFFT
+    fft_run<L, true, STORE_LAST, 0, 0, V3X>(z, tile, twl, tw0, lane);
+#endif
 }
 
 }  // namespace pv

@@ -192,6 +192,8 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (
             // RACC: (p j_k mod q) / q as a float (exact: q <= 4096)
             jkl[i] = RACC ? __float_as_uint((float)p.jk_mod[i] * p.inv_q) : p.jk_mod[i];
             if (MODE == 2) { srcl[2 * i] = p.src_first[i]; srcl[2 * i + 1] = p.src_cnt[i]; }
+            // MODE 3: the source's byte offset in a wave's tile, L + 1 (zero slot) if none
+            if (MODE == 3) srcl[i] = (int)sizeof(float2) * (p.src_first[i] >= 0 ? p.src_first[i] : L + 1);
         }
     }
     float* ring = rings + w * N;  // ROLA: the run's tail, written after the frame loop
@@ -467,13 +469,17 @@ bool synthesis_lane_kernel(int L, int mode, int hs, bool q_pow2, unsigned long l
     return mode != 1 && qp && syn_dt(L, hs) != 0;
 }
 
-// mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT
+// mode: 0 STANDARD stretch, 2 STANDARD pitch, 1 REF_COMPAT (the kernels' MODE 3: pitch >= 1)
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s) {
     dim3 grid((p.nruns + 3) / 4, channels);
     const bool qp = p.q_pow2 && p.q <= 4096ull;
     const int dt = (mode == 1 || qp) ? syn_dt(L, p.hs) : 0;
     if (mode == 0) return qp ? launch_synthesis_mode<0, true>(L, dt, grid, p, s)
                              : launch_synthesis_mode<0, false>(L, dt, grid, p, s);
+    // pitch ratio >= 1: at most one source per bin, the gather fixed at compile time (MODE 3:
+    // the per-bin source-count loops of ratios < 1 are not in the frame loop; config 4)
+    if (mode == 2 && p.rho >= 1.0f) return qp ? launch_synthesis_mode<3, true>(L, dt, grid, p, s)
+                                              : launch_synthesis_mode<3, false>(L, dt, grid, p, s);
     if (mode == 2) return qp ? launch_synthesis_mode<2, true>(L, dt, grid, p, s)
                              : launch_synthesis_mode<2, false>(L, dt, grid, p, s);
     return launch_synthesis_mode<1, false>(L, dt, grid, p, s);

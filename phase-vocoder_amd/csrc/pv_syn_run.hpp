@@ -301,7 +301,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     // (2 waves per SIMD are set by LDS, so VGPRs up to 256 cost no occupancy) and the L = 512
     // per-lane kernels (within their 3 waves/SIMD budget)
     // (not the L = 512 pitch kernel with out hop 128: with the contract-v3 FFT it would spill)
-    using TwS = typename std::conditional<((L == 1024 || (L == 512 && LANEK && !(MODE == 2 && DT == 1))) && ROLA),
+    using TwS = typename std::conditional<((L == 1024 || (L == 512 && LANEK && !(MODE >= 2 && DT == 1))) && ROLA),
                                           TwReg<E>, NoTwReg>::type;
     TwS twr;
     if constexpr (TwS::ON) {
@@ -309,10 +309,12 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         for (int q = 0; q < E; ++q) twr.v[q] = lds_ld(&sc.twsl[lane + 64 * q]);
     }
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
-    auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E]) {
+    auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hk) {
         const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
-        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, NoHook, TwS>(sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile,
-                                                                           lane, z, ekr, jkr, NoHook{}, twr);
+        using H = std::decay_t<decltype(hk)>;
+        // (L = 1024: the radix-16/16/4 inverse FFT on the v3 pass table, p.tw)
+        synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, H, TwS, (L == 1024)>(
+            sv, u > 0, tq, M, phprev, pmap, stb, tw0, tile, lane, z, ekr, jkr, hk, twr);
     };
     // PV_SPEC_PACKED rows: lane 0 finds bins 0 and L in slot 0 (the row has no slot L)
     const bool packed = p.packed != 0;
@@ -368,7 +370,7 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
             for (int i = 0; i <= E; ++i) sv[i] = make_float2(row[i].x, row[i].y);
             unpack(sv);
             float2 z[E];
-            synth(u, t0 + u, sv, z);
+            synth(u, t0 + u, sv, z, NoHook{});
             ola_regs(z);
             flush_regs(u, std::true_type{});  // exactly D stores
         };
@@ -385,6 +387,11 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
             vm_wait<D>(ra);
         }
     } else {
+        // L >= 1024 (ROLA): the next row's loads are issued once the frame has consumed the
+        // current row (synth_frame's hook, before the pre-step), into the same registers —
+        // no copy of the row (34 VGPR moves per frame); the loads have the inverse FFT and
+        // the overlap-add to land
+        constexpr bool LATE = ROLA && L >= 1024 && MODE != 2;  // (MODE 2: 260 VGPRs, 1 wave/SIMD)
         const bool fast_st = ROLA && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
         (void)fast_st;
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
@@ -397,13 +404,21 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         for (int u = 0; u < p.F; ++u) {
             const int t = t0 + u;
             if (u < nfr) {
+                float2 z[E];
+                if constexpr (LATE) {
+                    unpack(sv);
+                    // (unconditional: the run's last frame re-reads its own row, so the
+                    // registers take no merge of loaded and kept values)
+                    const int tn = (u + 1 < nfr) ? t + 1 : t;
+                    synth(u, t, sv, z, [&]() { load_row(specc + (long long)tn * p.spec_stride); });
+                } else {
                 float2 cur[E + 1];
 #pragma unroll
                 for (int i = 0; i <= E; ++i) cur[i] = sv[i];
                 unpack(cur);  // at use: unpacking at the load would wait for it at once
                 if (u + 1 < nfr) load_row(specc + (long long)(t + 1) * p.spec_stride);
-                float2 z[E];
-                synth(u, t, cur, z);
+                synth(u, t, cur, z, NoHook{});
+                }
                 if constexpr (ROLA) {
                     ola_regs(z);
                     // the next row has had the whole frame to land: wait for it here, before

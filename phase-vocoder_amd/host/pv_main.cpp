@@ -29,6 +29,7 @@
 // output is 16-bit stereo of timeScale*n samples (main.cpp:140-143).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -59,7 +60,10 @@ static int callback(void* outputBuffer, void* inputBuffer, unsigned int nBufferF
     if (status) std::printf("Stream underflow detected!\n");
     std::memcpy(pv->curr_input, inputBuffer, sizeof(float) * nBufferFrames);  // main.cpp:53
     pv->analysis();                                                            // main.cpp:54
-    std::memcpy(outputBuffer, pv->prev_output, sizeof(float) * pv->rtOutputSamples());
+    // the buffer's emitted samples, never more than the device buffer holds (main() rejects
+    // an RT run whose buffers emit more than they take: a stretch above 1)
+    const unsigned int n = std::min<unsigned int>((unsigned int)pv->rtOutputSamples(), nBufferFrames);
+    std::memcpy(outputBuffer, pv->prev_output, sizeof(float) * n);
     return 0;
 }
 
@@ -129,6 +133,11 @@ int main(int argc, char** argv) {
     if (rt) {
         // main.cpp:84-101 + RT block: buffers of bufferSize = nSamps frames of channel 0
         const unsigned int bufferSize = phase.nSamps;
+        if (phase.rtOutputSamples() > (int)bufferSize) {
+            std::fprintf(stderr, "err: --rt emits %d samples per %u-sample buffer (scale > 1); an RtAudio "
+                         "output buffer holds %u\n", phase.rtOutputSamples(), bufferSize, bufferSize);
+            return 1;
+        }
         std::vector<float> inBuf(bufferSize), outBuf((size_t)std::max(phase.rtOutputSamples(), 1));
         std::printf("Real-time callbacks\n");
         int outIndex = 0;

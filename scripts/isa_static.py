@@ -31,7 +31,7 @@ KERNELS = {
     ("c3", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi512ELb0ELi2ELb1E", 9),
     ("c3", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi0ELi1ELb1ELb1E", 17),
     ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1E", 17),
-    ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi2ELi4ELb1ELb1E", 33),
+    ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
 }
