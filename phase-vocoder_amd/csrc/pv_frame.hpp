@@ -346,19 +346,25 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
                     if constexpr (i <= E) o[decltype(jj)::value] = lds_ld(&srco[(i == E) ? L : lane + 64 * i]);
                 });
             };
+            // (L >= 1024: the next group's offsets are read while this group computes; at
+            // L <= 512 the kernels sit at their VGPR budgets, one group at a time)
             unsigned on[G];
-            offs_reads(std::integral_constant<int, 0>{}, on);
+            if constexpr (L >= 1024) offs_reads(std::integral_constant<int, 0>{}, on);
             static_for<0, NGRP>([&](auto ig) {
                 constexpr int i0 = decltype(ig)::value * G;
                 unsigned o[G];
                 float2 f[G];
+                if constexpr (L >= 1024) {
 #pragma unroll
-                for (int j = 0; j < G; ++j) o[j] = on[j];
+                    for (int j = 0; j < G; ++j) o[j] = on[j];
+                } else {
+                    offs_reads(ig, o);
+                }
                 static_for<0, G>([&](auto jj) {
                     constexpr int j = decltype(jj)::value;
                     if constexpr (i0 + j <= E) f[j] = lds_ld(reinterpret_cast<const float2*>(tb + o[j]));
                 });
-                if constexpr (decltype(ig)::value + 1 < NGRP)
+                if constexpr (L >= 1024 && decltype(ig)::value + 1 < NGRP)
                     offs_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, on);
                 static_for<0, G>([&](auto jj) {
                     constexpr int j = decltype(jj)::value;

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
             if (i < B) {
                 tts[k] = p.tws[i];
                 if (MODE == 2) { tsf[k] = p.src_first[i]; tsc[k] = p.src_cnt[i]; }
+                if (MODE == 3) tsf[k] = p.src_first[i];
             }
         }
 #pragma unroll
@@ -163,6 +164,8 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
             if (i < B) {
                 twsl[i] = tts[k];
                 if (MODE == 2) { srcl[2 * i] = tsf[k]; srcl[2 * i + 1] = tsc[k]; }
+                // MODE 3 (pitch >= 1): the source's byte offset in a wave's tile, zero slot L + 1
+                if (MODE == 3) srcl[i] = (int)sizeof(float2) * (tsf[k] >= 0 ? tsf[k] : L + 1);
             }
         }
 #pragma unroll
@@ -321,10 +324,12 @@ static hipError_t launch_fused_m(int L, int dt, dim3 grid, const FusedParams& p,
     }
 }
 
-// mode: 0 STANDARD stretch, 2 STANDARD pitch (q = 1 only; the caller checks)
+// mode: 0 STANDARD stretch, 2 STANDARD pitch (q = 1 only; the caller checks); pitch >= 1
+// takes the MODE 3 kernels (one source per bin: the select-free gather, as k_synthesis)
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s) {
     const dim3 grid((p.nruns + 3) / 4, channels);
     const int dt = p.hs / 128;
+    if (mode == 2 && p.rho >= 1.0f) return launch_fused_m<3>(L, dt, grid, p, s);
     return mode == 2 ? launch_fused_m<2>(L, dt, grid, p, s) : launch_fused_m<0>(L, dt, grid, p, s);
 }
 
