@@ -72,6 +72,16 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     constexpr int N = 2 * L;
     constexpr int CH = kAnaChunk;
     constexpr int NST = row_stores<E, PACKED>();
+    // (PV_ABL_*: diagnostic timing-only ablations for A/B runs, wrong outputs: NOSTORE drops
+    // the row stores (the magnitudes go to a sink so that they are still computed), NOATAN
+    // the atan2, NOFFT the forward transform, NOWIN the window's LDS reads, L2IN the input's
+    // HBM reads: every frame re-reads the run's first frame)
+#ifdef PV_ABL_NOSTORE
+    constexpr int NSTW = 0;
+    float sink = 0.0f;
+#else
+    constexpr int NSTW = NST;
+#endif
     static_assert(!PACKED || CH >= 2, "packed rows: bins 0 and L in one chunk");
     const int BP = p.bins_pad;
     const float2* twl = lt.twl;
@@ -91,7 +101,12 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
 #pragma unroll
         for (int q = 0; q < E; ++q) {
+#ifdef PV_ABL_NOWIN
+            const float2 wv = make_float2(1.0f, 1.0f);
+            (void)wl;
+#else
             const float2 wv = lds_ld(&wl[64 * q]);  // window samples 2 (lane + 64 q) + {0,1}
+#endif
             z[q].x = xr[q].x * wv.x;
             z[q].y = xr[q].y * wv.y;
         }
@@ -100,7 +115,9 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
         (void)srow;
         // the last pass's registers feed the split directly (no final image in LDS)
+#ifndef PV_ABL_NOFFT
         fft_run<L, false, false, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
+#endif
         // bin L first (the packed slot 0 pairs it with bin 0): it is real, so its contract
         // phase is +0 or pi and needs no atan2 — computed once, wave-uniformly, instead of as
         // a ninth generic bin on every lane (bin_l_real)
@@ -127,7 +144,11 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             float phs[CH];
             static_for<0, CH / 2>([&](auto jj) {
                 constexpr int j = 2 * decltype(jj)::value;
+#ifdef PV_ABL_NOATAN
+                const f2v ph2 = f2v{X[j].y, X[j + 1].y};
+#else
                 const f2v ph2 = atan2_pv2(X[j].y, X[j].x, X[j + 1].y, X[j + 1].x);
+#endif
                 phs[j] = ph2.x;
                 phs[j + 1] = ph2.y;
             });
@@ -142,7 +163,12 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                     // the phase, which drives the unwrap decisions, stays bit-exact.  X
                     // came out doubled (split_chunk_bp TWICE): halve the magnitude.
                     const float mag = 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+#ifdef PV_ABL_NOSTORE
+                    sink += mag;
+                    if constexpr (false) {
+#else
                     if constexpr (PACKED && i == 0) {
+#endif
                         // slot 0: lane 0 carries bins 0 and L (both real), the others bin lane
                         const f2v s0 = (lane == 0) ? f2v{pack_real_bin(mag, ph), pack_real_bin(magL, phL)}
                                                    : f2v{mag, ph};
@@ -150,7 +176,11 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                     } else {
                         __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
                     }
+#ifdef PV_ABL_NOSTORE
+                    if constexpr (false) {
+#else
                     if constexpr (!PACKED && i == 0) {
+#endif
                         // bin L: the same value and address on every lane
                         __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
                     }
@@ -197,16 +227,25 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             float2 xr[E], z[E];
             load_fast(0, xr);
             window(xr, z);
-            for (int u = 0; u < ufast; ++u) {
-                f2v xv[D];  // the D new pairs of frame u+1: registers E-D .. E-1
-                gload_tail<D, E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
-                frame(u, z);  // exactly NST row stores (+ records at u = 0)
-                vm_wait<NST>(xv);
+#ifdef PV_ABL_L2IN
+            // (timing only: every frame re-reads the run's first frame, an L2 hit)
+            auto src = [&](int u) { (void)u; return xc + (long long)t0 * p.hop + 2 * lane; };
+#else
+            auto src = [&](int u) { return xc + (long long)(t0 + min(u, ufast - 1)) * p.hop + 2 * lane; };
+#endif
+            auto consume = [&](const f2v (&xv)[D]) {
 #pragma unroll
                 for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
 #pragma unroll
                 for (int j = 0; j < D; ++j) xr[E - D + j] = make_float2(xv[j].x, xv[j].y);
                 window(xr, z);
+            };
+            for (int u = 0; u < ufast; ++u) {
+                f2v xv[D];  // the D new pairs of frame u+1: registers E-D .. E-1
+                gload_tail<D, E>(xv, src(u + 1));
+                frame(u, z);  // exactly NST row stores (+ records at u = 0)
+                vm_wait<NSTW>(xv);
+                consume(xv);
             }
         }
     } else if (L <= 1024 && ufast > 0) {
@@ -220,7 +259,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             f2v xv[E];
             gload_pairs<E>(xv, xc + (long long)(t0 + min(u + 1, ufast - 1)) * p.hop + 2 * lane);
             frame(u, z);  // exactly NST row stores
-            vm_wait<NST>(xv);
+            vm_wait<NSTW>(xv);
             float2 xr[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) xr[q] = make_float2(xv[q].x, xv[q].y);
@@ -244,6 +283,9 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     }
     if (rec != nullptr)
         PV_FOR_BINS(E, lane, { rec[k] = decision_sum(sacc[i], nfr - 1); rec[2 * BP + k] = __float_as_int(phprev[i]); })
+#ifdef PV_ABL_NOSTORE
+    if (sink == 1234.5f && rec != nullptr) rec[lane] = 0;  // keeps the magnitudes computed
+#endif
 }
 
 }  // namespace pv
