@@ -465,7 +465,11 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         } else {
             PV_FOR_BINS(E, lane, {
                 float sn, cs;
+#ifdef PV_ABL_NOSINCOS
+                sn = phc[i]; cs = 1.0f - phc[i];
+#else
                 sincos_rev(phc[i], &sn, &cs);
+#endif
                 float2 y = make_float2(mag[i] * cs, mag[i] * sn);
                 if (k == 0 || k == L) y.y = 0.0f;
                 Yr[i] = y;

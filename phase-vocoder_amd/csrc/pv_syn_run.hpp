@@ -363,7 +363,12 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         // every store of the run is in bounds: trip u = [load row u+1] [frame u] [D stores]
         // [vmcnt(D): row u+1 landed, the stores may still be in flight].  Two row buffers
         // alternate (F is even), so no register copies carry a row across trips.
+#ifdef PV_ABL_L2ROWS
+        // (timing only: every frame re-reads the run's first row, an L2 hit)
+        auto rowp = [&](int u) { (void)u; return specc + (long long)t0 * p.spec_stride; };
+#else
         auto rowp = [&](int u) { return specc + (long long)(t0 + min(u, p.F - 1)) * p.spec_stride; };
+#endif
         auto step = [&](int u, const f2v (&row)[E + 1]) {
             float2 sv[E + 1];
 #pragma unroll
