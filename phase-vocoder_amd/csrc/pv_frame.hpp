@@ -173,6 +173,24 @@ __device__ __forceinline__ void bin_l_real(const float2 (&v)[Geo<L>::E], const f
     phL = (Xr < 0.0f) ? kPi : 0.0f;
 }
 
+// bin_l_real from the natural-order image in LDS (the fused kernel's split reads the tile):
+// Z[0] = tile[0], the same address on every lane
+template <int L, bool TWICE>
+__device__ __forceinline__ void bin_l_real_tile(const float2* tile, const float2* twsl, float& magL, float& phL) {
+    const float2 z0 = lds_ld(tile);
+    const float ax = z0.x, ay = z0.y;
+    const float2 tw = lds_ld(&twsl[L]);
+    constexpr float h = TWICE ? 1.0f : 0.5f;
+    const float er = h * (ax + ax);
+    const float orr = h * (ay + ay);
+    const float oi = h * (ax - ax);
+    const float Xr = __builtin_fmaf(orr, tw.x, __builtin_fmaf(-oi, tw.y, er));  // contract v2
+    const float zero = 0.0f;
+    const float m = __builtin_amdgcn_sqrtf(__builtin_fmaf(Xr, Xr, zero * zero));
+    magL = TWICE ? 0.5f * m : m;
+    phL = (Xr < 0.0f) ? kPi : 0.0f;
+}
+
 // bins of a lane: k = lane + 64 i (i < E), plus k = L on lane 0 (i == E)
 #define PV_FOR_BINS(E_, lane_, ...)                              \
     _Pragma("unroll") for (int i = 0; i <= (E_); ++i) {          \

@@ -196,33 +196,37 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
             fft_run<L, false, true>(z, tile, twl, tw0, lane);
             float2 sv[E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
-            // bins in pairs: the phases of a pair through the packed-fp32 atan2 (atan2_pv2,
-            // bit-identical to atan2_pv per half)
+            // bin L (real: A = B = Z[0]) once, wave-uniformly, as k_std_analysis's bin_l_real:
+            // its contract phase is +0 or pi, no atan2 (bit-identical to the generic bin)
+            {
+                float magL, phL;
+                bin_l_real_tile<L, true>(tile, twsl, magL, phL);
+                sv[E] = make_float2(magL, phL);
+                if (!p.packed) __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
+            }
+            // bins 0 .. E-1 in pairs: the phases of a pair through the packed-fp32 atan2
+            // (atan2_pv2, bit-identical to atan2_pv per half)
             constexpr int CH = 2;
-            static_for<0, (E + CH) / CH>([&](auto ic) {
+            static_for<0, E / CH>([&](auto ic) {
                 constexpr int i0 = decltype(ic)::value * CH;
                 float2 X[CH];
                 split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
                 float phs[CH];
-                if constexpr (i0 + 1 <= E) {
+                {
                     const f2v ph2 = atan2_pv2(X[0].y, X[0].x, X[1].y, X[1].x);
                     phs[0] = ph2.x;
                     phs[1] = ph2.y;
-                } else {
-                    phs[0] = atan2_pv(X[0].y, X[0].x);
                 }
                 static_for<0, CH>([&](auto cc) {
                     constexpr int c2 = decltype(cc)::value;
                     constexpr int i = i0 + c2;
-                    if constexpr (i <= E) {
+                    {
                         const float ph = phs[c2];
                         float mag = __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
                         mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
                         sv[i] = make_float2(mag, ph);
-                        // bin L (i = E): the same value and address on every lane (natural
-                        // layout only; packed rows carry it in slot 0); bins 0..63 go out below
-                        if (i > 0 && (i < E || !p.packed))
-                            __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[(i == E) ? L - lane : 64 * i]));
+                        // bins 0..63 go out below (slot 0)
+                        if (i > 0) __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
                     }
                 });
             });
