@@ -186,6 +186,12 @@ def test_ragged_channel_strides_and_determinism(cuda):
     (256, 4, TIME_SHIFT, 1.0),     # out hop 64: LDS ring overlap-add
     (1024, 4, TIME_SHIFT, 0.75),   # out hop 192: LDS ring overlap-add
     (2048, 8, TIME_SHIFT, 1.0),    # L=1024, out hop 256
+    # pitch >= 1 takes the MODE 3 kernels (one source per bin, byte-offset map, zero slot)
+    (2048, 4, PITCH_SHIFT, 1.0),   # L=1024: every bin its own source
+    (2048, 4, PITCH_SHIFT, 2.0),   # L=1024, q = 1: odd bins sourceless (zero slot); single launch
+    (2048, 8, PITCH_SHIFT, 1.25),  # L=1024, out hop 256 (DT = 2)
+    (1024, 4, PITCH_SHIFT, 1.0),   # L=512
+    (1024, 3, PITCH_SHIFT, 1.5),   # L=512, hop 341: LDS ring overlap-add (DT = 0)
 ])
 def test_std_process_parity_geometries(cuda, N, hop_div, effect, scale):
     """Both overlap-add paths (registers when the out hop is a multiple of 128 and
