@@ -342,138 +342,138 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
 #endif
             float2 Y[E + 1];
             if constexpr (MODE == 3) {
-            // at most one source per bin (pitch ratio >= 1): srcl holds each bin's source as a
-            // byte offset into the tile, slot L + 1 (a zero written here every frame) when no
-            // source maps there.  Every lane gathers every bin, bin L included (lanes != 0
-            // read bin L's source too and ignore it: no exec-masked blocks), and no selects:
-            // 4-byte map reads, one tile read and the sin/cos per bin.
-            PV_FOR_BINS(E, lane, { if (i < E) tile[k] = make_float2(mag[i], phc[i]); })
-            {
-                // bin L from lane 0, the zero slot from the others (one store, no branch)
-                const bool l0 = lane == 0;
-                tile[l0 ? L : L + 1] = make_float2(l0 ? mag[E] : 0.0f, l0 ? phc[E] : 0.0f);
-            }
-            wave_lds_sync();
-            const unsigned* srco = reinterpret_cast<const unsigned*>(srcl);
-            const char* tb = reinterpret_cast<const char*>(tile);
-            constexpr int G = (L >= 1024) ? 4 : 1;
-            constexpr int NGRP = (E + G) / G;
-            auto offs_reads = [&](auto ig, unsigned (&o)[G]) {
-                static_for<0, G>([&](auto jj) {
-                    constexpr int i = decltype(ig)::value * G + decltype(jj)::value;
-                    if constexpr (i <= E) o[decltype(jj)::value] = lds_ld(&srco[(i == E) ? L : lane + 64 * i]);
-                });
-            };
-            // (L >= 1024: the next group's offsets are read while this group computes; at
-            // L <= 512 the kernels sit at their VGPR budgets, one group at a time)
-            unsigned on[G];
-            if constexpr (L >= 1024) offs_reads(std::integral_constant<int, 0>{}, on);
-            static_for<0, NGRP>([&](auto ig) {
-                constexpr int i0 = decltype(ig)::value * G;
-                unsigned o[G];
-                float2 f[G];
-                if constexpr (L >= 1024) {
-#pragma unroll
-                    for (int j = 0; j < G; ++j) o[j] = on[j];
-                } else {
-                    offs_reads(ig, o);
+                // at most one source per bin (pitch ratio >= 1): srcl holds each bin's source as a
+                // byte offset into the tile, slot L + 1 (a zero written here every frame) when no
+                // source maps there.  Every lane gathers every bin, bin L included (lanes != 0
+                // read bin L's source too and ignore it: no exec-masked blocks), and no selects:
+                // 4-byte map reads, one tile read and the sin/cos per bin.
+                PV_FOR_BINS(E, lane, { if (i < E) tile[k] = make_float2(mag[i], phc[i]); })
+                {
+                    // bin L from lane 0, the zero slot from the others (one store, no branch)
+                    const bool l0 = lane == 0;
+                    tile[l0 ? L : L + 1] = make_float2(l0 ? mag[E] : 0.0f, l0 ? phc[E] : 0.0f);
                 }
-                static_for<0, G>([&](auto jj) {
-                    constexpr int j = decltype(jj)::value;
-                    if constexpr (i0 + j <= E) f[j] = lds_ld(reinterpret_cast<const float2*>(tb + o[j]));
-                });
-                if constexpr (L >= 1024 && decltype(ig)::value + 1 < NGRP)
-                    offs_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, on);
-                static_for<0, G>([&](auto jj) {
-                    constexpr int j = decltype(jj)::value;
-                    if constexpr (i0 + j <= E) {
-                        float sn, cs;
-                        sincos_rev(f[j].y, &sn, &cs);
-                        Y[i0 + j] = make_float2(f[j].x * cs, f[j].x * sn);
-                    }
-                });
-            });
-            } else {
-            PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
-            wave_lds_sync();
-            // {first source, count} in one 8-byte read; the first source's {mag, phase}
-            // in one read, without a branch (zero when no source maps here); more sources
-            // (ratios < 1) are summed in order like the oracle.  The ratio test is hoisted
-            // out of the bin loop (wave-uniform): inside it the compiler merges it with the
-            // per-lane count test into an exec-masked branch per bin (17 at L = 1024).
-            // The LDS reads are issued in groups of G bins (all map reads, then all tile
-            // reads, then the arithmetic): the volatile LDS loads keep program order, so bin
-            // by bin every map read -> tile read pair would be two serialized LDS round trips
-            // per bin (34 per frame at L = 1024).
-            // (config 4 synthesis -2.5 %; 1 at L <= 512, whose kernels sit at their VGPR budget)
-            // At L >= 1024 the groups are software-pipelined: group g + 1's map reads are
-            // issued right after group g's tile reads, so they are in flight while group g
-            // computes and one LDS round trip per group is exposed instead of two.
-            constexpr int G = (L >= 1024) ? 4 : 1;
-            constexpr int NGRP = (E + G) / G;
-            auto map_reads = [&](auto ig, i2v (&sc)[G]) {
-                constexpr int i0 = decltype(ig)::value * G;
-                static_for<0, G>([&](auto jj) {
-                    constexpr int j = decltype(jj)::value;
-                    constexpr int i = i0 + j;
-                    if constexpr (i <= E) {
-                        const int k = (i == E) ? L : lane + 64 * i;
-                        if (i < E || lane == 0) sc[j] = lds_ld2i(&srcl[2 * k]);
-                    }
-                });
-            };
-            auto gather = [&](auto multi_tag) {
-                constexpr bool MULTI = decltype(multi_tag)::value;
-                i2v scn[G];  // the next group's map entries (in flight)
-                if constexpr (L >= 1024) map_reads(std::integral_constant<int, 0>{}, scn);
+                wave_lds_sync();
+                const unsigned* srco = reinterpret_cast<const unsigned*>(srcl);
+                const char* tb = reinterpret_cast<const char*>(tile);
+                constexpr int G = (L >= 1024) ? 4 : 1;
+                constexpr int NGRP = (E + G) / G;
+                auto offs_reads = [&](auto ig, unsigned (&o)[G]) {
+                    static_for<0, G>([&](auto jj) {
+                        constexpr int i = decltype(ig)::value * G + decltype(jj)::value;
+                        if constexpr (i <= E) o[decltype(jj)::value] = lds_ld(&srco[(i == E) ? L : lane + 64 * i]);
+                    });
+                };
+                // (L >= 1024: the next group's offsets are read while this group computes; at
+                // L <= 512 the kernels sit at their VGPR budgets, one group at a time)
+                unsigned on[G];
+                if constexpr (L >= 1024) offs_reads(std::integral_constant<int, 0>{}, on);
                 static_for<0, NGRP>([&](auto ig) {
                     constexpr int i0 = decltype(ig)::value * G;
-                    i2v sc[G];
+                    unsigned o[G];
                     float2 f[G];
-        #ifdef PV_LANE0_PRESEL
-            if constexpr (true) {
-#else
-            if constexpr (L >= 1024) {
-#endif
+                    if constexpr (L >= 1024) {
 #pragma unroll
-                        for (int j = 0; j < G; ++j) sc[j] = scn[j];
+                        for (int j = 0; j < G; ++j) o[j] = on[j];
                     } else {
-                        map_reads(ig, sc);
+                        offs_reads(ig, o);
                     }
                     static_for<0, G>([&](auto jj) {
                         constexpr int j = decltype(jj)::value;
-                        constexpr int i = i0 + j;
-                        if constexpr (i <= E) {
-                            const int sidx = sc[j].x;
-                            if (i < E || lane == 0) f[j] = lds_ld(&tile[G_::pad(sidx >= 0 ? sidx : 0)]);
-                        }
+                        if constexpr (i0 + j <= E) f[j] = lds_ld(reinterpret_cast<const float2*>(tb + o[j]));
                     });
                     if constexpr (L >= 1024 && decltype(ig)::value + 1 < NGRP)
-                        map_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, scn);
+                        offs_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, on);
+                    static_for<0, G>([&](auto jj) {
+                        constexpr int j = decltype(jj)::value;
+                        if constexpr (i0 + j <= E) {
+                            float sn, cs;
+                            sincos_rev(f[j].y, &sn, &cs);
+                            Y[i0 + j] = make_float2(f[j].x * cs, f[j].x * sn);
+                        }
+                    });
+                });
+            } else {
+                PV_FOR_BINS(E, lane, { tile[G_::pad(k)] = make_float2(mag[i], phc[i]); })
+                wave_lds_sync();
+                // {first source, count} in one 8-byte read; the first source's {mag, phase}
+                // in one read, without a branch (zero when no source maps here); more sources
+                // (ratios < 1) are summed in order like the oracle.  The ratio test is hoisted
+                // out of the bin loop (wave-uniform): inside it the compiler merges it with the
+                // per-lane count test into an exec-masked branch per bin (17 at L = 1024).
+                // The LDS reads are issued in groups of G bins (all map reads, then all tile
+                // reads, then the arithmetic): the volatile LDS loads keep program order, so bin
+                // by bin every map read -> tile read pair would be two serialized LDS round trips
+                // per bin (34 per frame at L = 1024).
+                // (config 4 synthesis -2.5 %; 1 at L <= 512, whose kernels sit at their VGPR budget)
+                // At L >= 1024 the groups are software-pipelined: group g + 1's map reads are
+                // issued right after group g's tile reads, so they are in flight while group g
+                // computes and one LDS round trip per group is exposed instead of two.
+                constexpr int G = (L >= 1024) ? 4 : 1;
+                constexpr int NGRP = (E + G) / G;
+                auto map_reads = [&](auto ig, i2v (&sc)[G]) {
+                    constexpr int i0 = decltype(ig)::value * G;
                     static_for<0, G>([&](auto jj) {
                         constexpr int j = decltype(jj)::value;
                         constexpr int i = i0 + j;
                         if constexpr (i <= E) {
-                            if (i < E || lane == 0) {
-                                const int sidx = sc[j].x;
-                                float ms = (sidx >= 0) ? f[j].x : 0.0f;
-                                const float pc = (sidx >= 0) ? f[j].y : 0.0f;
-                                if constexpr (MULTI)
-                                    for (int qq = 1; qq < sc[j].y; ++qq) ms += tile[G_::pad(sidx + qq)].x;
-                                float sn, cs;
-                                sincos_rev(pc, &sn, &cs);
-                                Y[i] = make_float2(ms * cs, ms * sn);
-                            }
+                            const int k = (i == E) ? L : lane + 64 * i;
+                            if (i < E || lane == 0) sc[j] = lds_ld2i(&srcl[2 * k]);
                         }
                     });
-                });
-            };
-            if (pm.multi) {
-                gather(std::true_type{});
-            } else {
-                gather(std::false_type{});
-            }
-            }  // MODE 2
+                };
+                auto gather = [&](auto multi_tag) {
+                    constexpr bool MULTI = decltype(multi_tag)::value;
+                    i2v scn[G];  // the next group's map entries (in flight)
+                    if constexpr (L >= 1024) map_reads(std::integral_constant<int, 0>{}, scn);
+                    static_for<0, NGRP>([&](auto ig) {
+                        constexpr int i0 = decltype(ig)::value * G;
+                        i2v sc[G];
+                        float2 f[G];
+            #ifdef PV_LANE0_PRESEL
+                if constexpr (true) {
+#else
+                if constexpr (L >= 1024) {
+#endif
+#pragma unroll
+                            for (int j = 0; j < G; ++j) sc[j] = scn[j];
+                        } else {
+                            map_reads(ig, sc);
+                        }
+                        static_for<0, G>([&](auto jj) {
+                            constexpr int j = decltype(jj)::value;
+                            constexpr int i = i0 + j;
+                            if constexpr (i <= E) {
+                                const int sidx = sc[j].x;
+                                if (i < E || lane == 0) f[j] = lds_ld(&tile[G_::pad(sidx >= 0 ? sidx : 0)]);
+                            }
+                        });
+                        if constexpr (L >= 1024 && decltype(ig)::value + 1 < NGRP)
+                            map_reads(std::integral_constant<int, decltype(ig)::value + 1>{}, scn);
+                        static_for<0, G>([&](auto jj) {
+                            constexpr int j = decltype(jj)::value;
+                            constexpr int i = i0 + j;
+                            if constexpr (i <= E) {
+                                if (i < E || lane == 0) {
+                                    const int sidx = sc[j].x;
+                                    float ms = (sidx >= 0) ? f[j].x : 0.0f;
+                                    const float pc = (sidx >= 0) ? f[j].y : 0.0f;
+                                    if constexpr (MULTI)
+                                        for (int qq = 1; qq < sc[j].y; ++qq) ms += tile[G_::pad(sidx + qq)].x;
+                                    float sn, cs;
+                                    sincos_rev(pc, &sn, &cs);
+                                    Y[i] = make_float2(ms * cs, ms * sn);
+                                }
+                            }
+                        });
+                    });
+                };
+                if (pm.multi) {
+                    gather(std::true_type{});
+                } else {
+                    gather(std::false_type{});
+                }
+            }  // MODE 2 (several sources per bin)
             wave_lds_sync();
             PV_FOR_BINS(E, lane, {
                 float2 y = Y[i];
