@@ -254,6 +254,31 @@ static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hi
     return hipGetLastError();
 }
 
+// workgroups of the STANDARD analysis kernel launch_std_analysis picks for an aligned input
+// (hop = 128 d when that divides) that one CU holds at once; 0 if the runtime cannot say
+template <bool PK>
+static int std_analysis_wgs_per_cu_t(int L, int hop, bool ek_lane) {
+    int n = 0;
+    if (L != 128 && L != 256 && L != 512 && L != 1024 && L != 2048) return 0;
+    auto occ = [&](const void* k, size_t lds) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, lds) != hipSuccess) n = 0;
+    };
+    PV_DISPATCH_L(L, {
+        const int d = (hop % 128 == 0) ? hop / 128 : 0;
+        if (ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
+            constexpr int E_ = LL / 64;
+            if (d == 1) occ((const void*)k_std_analysis<LL, false, (1 < E_) ? 1 : 0, PK>, ana_lds_std<LL>(false));
+            else if (d == 2) occ((const void*)k_std_analysis<LL, false, (2 < E_) ? 2 : 0, PK>, ana_lds_std<LL>(false));
+            else occ((const void*)k_std_analysis<LL, false, (4 < E_) ? 4 : 0, PK>, ana_lds_std<LL>(false));
+        } else if (ek_lane) occ((const void*)k_std_analysis<LL, false, 0, PK>, ana_lds_std<LL>(false));
+        else occ((const void*)k_std_analysis<LL, true, 0, PK>, ana_lds_std<LL>(true));
+    });
+    return n;
+}
+int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed) {
+    return packed ? std_analysis_wgs_per_cu_t<true>(L, hop, ek_lane) : std_analysis_wgs_per_cu_t<false>(L, hop, ek_lane);
+}
+
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {
     const dim3 grid((p.nruns + 3) / 4, channels);
     return p.packed ? launch_std_analysis_t<true>(L, grid, p, s) : launch_std_analysis_t<false>(L, grid, p, s);

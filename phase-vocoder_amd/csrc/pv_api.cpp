@@ -593,6 +593,29 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     // 1024 channels x 861 frames: F = 24 / 32 / 40 / 48 / 64 -> 1.51-1.52 / 1.53-1.54 /
     // 1.47-1.48 / 1.49-1.50 / 1.46-1.49e8 frames/s)
     if (h->L_syn >= 1024 && F > 32) F = 32;
+    // Large STANDARD batches at L <= 512: the analysis grid runs in rounds of (workgroups one
+    // CU holds) x CUs, and a last partial round leaves most of the chip idle while its runs
+    // finish.  Among F = 48 .. 96 take the one with the fewest frame-times, rounds x F (ties:
+    // the shorter runs).  Config 3 (1024 x 1722 frames, 5 workgroups per CU, 256 CUs): 48
+    // gives 9216 workgroups = 8 rounds (the last a fifth full) x 48 = 384, 88 gives 5120 = 4
+    // x 88 = 352 (measured on two boxes: +1.7 / +1.8 % frames/s, profiles/r04_ab_c3_F.txt).
+    if (F == 48 && h->L_ana <= 512 && h->mode == PV_MODE_STANDARD) {
+        DeviceGuard g0(cfg->device);
+        int cus = 0;
+        const bool ekl = (64 % cfg->hop_div == 0 && h->bins >= 64);
+        const int wpc = pv::std_analysis_wgs_per_cu(h->L_ana, h->hop, ekl, h->packed != 0);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
+            cus > 0 && wpc > 0) {
+            const long long slots = (long long)cus * wpc;
+            const long long C = std::max(cfg->max_channels, 1), T = std::max(cfg->max_frames, 1);
+            long long best = -1;
+            for (int f = 48; f <= 96; f += 2) {
+                const long long wgs = C * (((T + f - 1) / f + 3) / 4);
+                const long long cost = ((wgs + slots - 1) / slots) * f;
+                if (best < 0 || cost < best) { best = cost; F = f; }
+            }
+        }
+    }
     // tuning override (even, 8..256): PV_RUN_FRAMES
     if (const char* ev = std::getenv("PV_RUN_FRAMES")) {
         const int f = std::atoi(ev);
