@@ -62,8 +62,8 @@ constexpr int row_stores() { return PACKED ? E : E + 1; }
 // another launch, long after they would have left the caches).  rec (nullable): the run
 // record {S, phi(t0), phi(t0 + nfr - 1)} (kRecFields rows of bins_pad words, phases as their
 // float bits).
-template <int L, bool EKL, int D, bool PACKED>
-__device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile,
+template <int L, bool EKL, int D, bool PACKED, int RING = 0>
+__device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile, float* ring,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
                                         float e_lane, int* rec, float (&phprev)[Geo<L>::E + 1],
                                         ana_acc_t<L> (&sacc)[Geo<L>::E + 1]) {
@@ -221,7 +221,59 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     // [vmcnt(NST): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
     // The prefetch index is clamped (the last trip reloads its own frame), so the loads
     // and stores are unconditional and the count is exact (gload_pairs / vm_wait).
-    if constexpr (D > 0) {
+    if constexpr (D > 0 && RING > 0) {
+        // LDS-DMA input ring (RING slots of hop samples per wave): frame v's hop new samples
+        // are one or two global_load_lds_dwordx4 (NDMA = hop / 256) into slot v mod RING,
+        // issued RING frames ahead of their use, so no VGPR holds samples in flight.
+        // Trip u: [frame u: NST row stores] [vmcnt: x(u+1) landed] [ds_read the lane's D
+        // pairs of x(u+1)] [window] [DMA x(u+1+RING) into the slot just read].  Ops issued
+        // after x(u+1): (RING-1) (NST + NDMA) + NST in the steady state, (RING-1) NDMA +
+        // (u+1) NST in the first trips (x(1..RING) issued before the loop) — the wait below
+        // uses that lower bound (extra record stores at u = 0 only make it conservative).
+        static_assert(D < E, "shifted input: hop < N / 2");
+        static_assert(D == 2 || D == 4, "the ring moves 1 KiB DMA pieces: hop = 256 or 512");
+        constexpr int NDMA = D / 2;
+        constexpr int HOPF = 128 * D;  // floats per slot
+        if (ufast > 0) {
+            float2 xr[E], z[E];
+            const unsigned rbase = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+            auto dma = [&](int v, int slot) {
+                const float* g = xc + (long long)(t0 + min(v, ufast - 1)) * p.hop + (N - HOPF) + 4 * lane;
+#pragma unroll
+                for (int j = 0; j < NDMA; ++j) glds16(g + 256 * j, rbase + (unsigned)(slot * HOPF + 256 * j) * 4u);
+            };
+            {
+                f2v x0[E];
+                gload_pairs<E>(x0, xc + (long long)t0 * p.hop + 2 * lane);
+#pragma unroll
+                for (int v = 1; v <= RING; ++v) dma(v, v % RING);
+                vm_wait<RING * NDMA>(x0);
+#pragma unroll
+                for (int q = 0; q < E; ++q) xr[q] = make_float2(x0[q].x, x0[q].y);
+                window(xr, z);
+            }
+            int slot = 1 % RING;  // slot of x(u + 1)
+            for (int u = 0; u < ufast; ++u) {
+                frame(u, z);  // exactly NST row stores (+ records at u = 0)
+                {
+                    const int m = min(u, RING - 1);
+                    static_for<0, RING>([&](auto mc) {
+                        constexpr int M = decltype(mc)::value;
+                        constexpr int K = (RING - 1) * NDMA + (M + 1) * NSTW;
+                        if (m == M) vm_wait_n<(K < 63 ? K : 63)>();
+                    });
+                }
+                const float* rs = ring + slot * HOPF + 2 * lane;
+#pragma unroll
+                for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) xr[E - D + j] = lds_ld(reinterpret_cast<const float2*>(rs + 128 * j));
+                window(xr, z);
+                dma(u + 1 + RING, slot);
+                slot = (slot + 1 == RING) ? 0 : slot + 1;
+            }
+        }
+    } else if constexpr (D > 0) {
         static_assert(D < E, "shifted input: hop < N / 2");
         if (ufast > 0) {
             float2 xr[E], z[E];

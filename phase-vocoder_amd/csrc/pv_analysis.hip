@@ -22,33 +22,53 @@ constexpr int kAnaWaves1024 = 3;
 // frame costs only its D new sample pairs per lane (the other E - D are shifted in
 // registers): 1/E of the frame's bytes leave L2 instead of all of them.
 // PACKED: the pv.h PV_SPEC_PACKED row layout (bin L folded into slot 0).
-template <int L, bool EKL, int D, bool PACKED>
-__global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
+// Input ring (PV_ANA_RING = R > 0, hop = 256 or 512): each wave streams its frames' new
+// samples R frames ahead into R LDS slots by LDS-DMA (ana_run); the workgroup is then W =
+// PV_ANA_WAVES waves sharing one copy of the tables (the ring's LDS is paid by the tables'
+// duplication across 4-wave workgroups instead of by occupancy).
+#ifndef PV_ANA_RING
+#define PV_ANA_RING 0
+#endif
+#ifndef PV_ANA_WAVES
+#define PV_ANA_WAVES 10
+#endif
+#ifndef PV_ANA_BIGWG
+#define PV_ANA_BIGWG 0
+#endif
+template <int L, int D>
+constexpr int ana_ring() { return (D == 2 && L == 512) ? PV_ANA_RING : 0; }
+template <int L, int D>
+constexpr int ana_waves() { return (ana_ring<L, D>() > 0 || (PV_ANA_BIGWG && D == 2 && L == 512)) ? PV_ANA_WAVES : 4; }
+
+template <int L, bool EKL, int D, bool PACKED, int W = ana_waves<L, D>(), int RING = ana_ring<L, D>()>
+__global__ __launch_bounds__(64 * W, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int B = L + 1;
+    constexpr int NT = 64 * W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int TWN = ana_twl_n<L>();
-    float2* twl = reinterpret_cast<float2*>(smem);   // TWN stage-major twiddles (L, or L/4)
+    float* rings = reinterpret_cast<float*>(smem);    // W x RING x hop samples (LDS-DMA ring)
+    float2* twl = reinterpret_cast<float2*>(rings + W * RING * 128 * D);  // TWN stage-major twiddles (L, or L/4)
     float2* twsl = twl + TWN;                         // L+1 split twiddles (+1 pad)
-    float2* tiles = twsl + (L + 2);                   // 4 x TILE
-    float* winl = reinterpret_cast<float*>(tiles + 4 * G_::TILE);  // N
+    float2* tiles = twsl + (L + 2);                   // W x TILE
+    float* winl = reinterpret_cast<float*>(tiles + W * G_::TILE);  // N
     float* ekl = winl + N;                            // B
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
     float2 tw0[Geo<L>::E];
     load_tw0<L>(tw0, p.tw);
-    for (int i = tid; i < TWN; i += 256) twl[i] = p.tw[i];
-    for (int i = tid; i < B; i += 256) {
+    for (int i = tid; i < TWN; i += NT) twl[i] = p.tw[i];
+    for (int i = tid; i < B; i += NT) {
         twsl[i] = p.tws[i];
         if (EKL) ekl[i] = p.ek[i];
     }
     const float e_lane = EKL ? 0.0f : p.ek[tid & 63];
-    for (int i = tid; i < N; i += 256) winl[i] = p.win[i];
+    for (int i = tid; i < N; i += NT) winl[i] = p.win[i];
     __syncthreads();
-    const int run = blockIdx.x * 4 + w, c = blockIdx.y;
+    const int run = blockIdx.x * W + w, c = blockIdx.y;
     if (run >= p.nruns) return;
     const int t0 = run * p.F;
     const int nfr = min(p.F, p.frames - t0);
@@ -57,8 +77,8 @@ __global__ __launch_bounds__(256, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad : nullptr;
     float phprev[E + 1];
     ana_acc_t<L> sacc[E + 1];
-    ana_run<L, EKL, D, PACKED>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c, t0, nfr,
-                               e_lane, rec, phprev, sacc);
+    ana_run<L, EKL, D, PACKED, RING>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, rings + w * RING * 128 * D,
+                                     tw0, lane, c, t0, nfr, e_lane, rec, phprev, sacc);
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT
@@ -217,9 +237,11 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
 
 
 // ------------------------------------------------------------------ launchers
-template <int L>
+template <int L, int D = 0>
 static size_t ana_lds_std(bool ekl) {
-    return sizeof(float2) * (ana_twl_n<L>() + (L + 2) + 4 * Geo<L>::TILE) + sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
+    constexpr int W = ana_waves<L, D>(), R = ana_ring<L, D>();
+    return sizeof(float) * W * R * 128 * D + sizeof(float2) * (ana_twl_n<L>() + (L + 2) + W * Geo<L>::TILE) +
+           sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
 }
 template <int L>
 static size_t ana_lds_compat() {
@@ -228,13 +250,13 @@ static size_t ana_lds_compat() {
 // twiddles + 4 tiles + 4 rings (tails) [+ gain] + ek/jk + pitch map; with register
 // overlap-add at L <= 512 the gains live in registers and gainl is not allocated
 
-#define PV_DISPATCH_L(L_, EXPR)                       \
+#define PV_DISPATCH_L(L_, ...)                        \
     switch (L_) {                                     \
-        case 128: { constexpr int LL = 128; EXPR; } break;   \
-        case 256: { constexpr int LL = 256; EXPR; } break;   \
-        case 512: { constexpr int LL = 512; EXPR; } break;   \
-        case 1024: { constexpr int LL = 1024; EXPR; } break; \
-        case 2048: { constexpr int LL = 2048; EXPR; } break; \
+        case 128: { constexpr int LL = 128; __VA_ARGS__; } break;   \
+        case 256: { constexpr int LL = 256; __VA_ARGS__; } break;   \
+        case 512: { constexpr int LL = 512; __VA_ARGS__; } break;   \
+        case 1024: { constexpr int LL = 1024; __VA_ARGS__; } break; \
+        case 2048: { constexpr int LL = 2048; __VA_ARGS__; } break; \
         default: return hipErrorInvalidValue;         \
     }
 
@@ -245,9 +267,14 @@ static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hi
         const int d = (p.aligned && p.hop % 128 == 0) ? p.hop / 128 : 0;
         if (p.ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
             constexpr int E_ = LL / 64;  // D < E (instantiated for every L, run for the checked ones)
-            if (d == 1) hipLaunchKernelGGL((k_std_analysis<LL, false, (1 < E_) ? 1 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-            else if (d == 2) hipLaunchKernelGGL((k_std_analysis<LL, false, (2 < E_) ? 2 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
-            else hipLaunchKernelGGL((k_std_analysis<LL, false, (4 < E_) ? 4 : 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
+            constexpr int D1 = (1 < E_) ? 1 : 0, D2 = (2 < E_) ? 2 : 0, D4 = (4 < E_) ? 4 : 0;
+            auto go = [&](auto kern, int W, size_t lds) {
+                const dim3 g((p.nruns + W - 1) / W, grid.y);
+                hipLaunchKernelGGL(kern, g, dim3(64 * W), lds, s, p);
+            };
+            if (d == 1) go(k_std_analysis<LL, false, D1, PK>, ana_waves<LL, D1>(), ana_lds_std<LL, D1>(false));
+            else if (d == 2) go(k_std_analysis<LL, false, D2, PK>, ana_waves<LL, D2>(), ana_lds_std<LL, D2>(false));
+            else go(k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
         } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false, 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
         else hipLaunchKernelGGL((k_std_analysis<LL, true, 0, PK>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });
@@ -255,28 +282,33 @@ static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hi
 }
 
 // workgroups of the STANDARD analysis kernel launch_std_analysis picks for an aligned input
-// (hop = 128 d when that divides) that one CU holds at once; 0 if the runtime cannot say
+// (hop = 128 d when that divides) that one CU holds at once (0 if the runtime cannot say),
+// and its waves per workgroup
 template <bool PK>
-static int std_analysis_wgs_per_cu_t(int L, int hop, bool ek_lane) {
+static int std_analysis_wgs_per_cu_t(int L, int hop, bool ek_lane, int* waves_per_wg) {
     int n = 0;
+    *waves_per_wg = 4;
     if (L != 128 && L != 256 && L != 512 && L != 1024 && L != 2048) return 0;
-    auto occ = [&](const void* k, size_t lds) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, lds) != hipSuccess) n = 0;
+        auto occ = [&](const void* k, int W, size_t lds) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * W, lds) != hipSuccess) n = 0;
+        *waves_per_wg = W;
     };
     PV_DISPATCH_L(L, {
         const int d = (hop % 128 == 0) ? hop / 128 : 0;
         if (ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
             constexpr int E_ = LL / 64;
-            if (d == 1) occ((const void*)k_std_analysis<LL, false, (1 < E_) ? 1 : 0, PK>, ana_lds_std<LL>(false));
-            else if (d == 2) occ((const void*)k_std_analysis<LL, false, (2 < E_) ? 2 : 0, PK>, ana_lds_std<LL>(false));
-            else occ((const void*)k_std_analysis<LL, false, (4 < E_) ? 4 : 0, PK>, ana_lds_std<LL>(false));
-        } else if (ek_lane) occ((const void*)k_std_analysis<LL, false, 0, PK>, ana_lds_std<LL>(false));
-        else occ((const void*)k_std_analysis<LL, true, 0, PK>, ana_lds_std<LL>(true));
+            constexpr int D1 = (1 < E_) ? 1 : 0, D2 = (2 < E_) ? 2 : 0, D4 = (4 < E_) ? 4 : 0;
+            if (d == 1) occ((const void*)k_std_analysis<LL, false, D1, PK>, ana_waves<LL, D1>(), ana_lds_std<LL, D1>(false));
+            else if (d == 2) occ((const void*)k_std_analysis<LL, false, D2, PK>, ana_waves<LL, D2>(), ana_lds_std<LL, D2>(false));
+            else occ((const void*)k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
+        } else if (ek_lane) occ((const void*)k_std_analysis<LL, false, 0, PK>, 4, ana_lds_std<LL>(false));
+        else occ((const void*)k_std_analysis<LL, true, 0, PK>, 4, ana_lds_std<LL>(true));
     });
     return n;
 }
-int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed) {
-    return packed ? std_analysis_wgs_per_cu_t<true>(L, hop, ek_lane) : std_analysis_wgs_per_cu_t<false>(L, hop, ek_lane);
+int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed, int* waves_per_wg) {
+    return packed ? std_analysis_wgs_per_cu_t<true>(L, hop, ek_lane, waves_per_wg)
+                  : std_analysis_wgs_per_cu_t<false>(L, hop, ek_lane, waves_per_wg);
 }
 
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s) {

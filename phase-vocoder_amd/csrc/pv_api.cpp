@@ -603,14 +603,15 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         DeviceGuard g0(cfg->device);
         int cus = 0;
         const bool ekl = (64 % cfg->hop_div == 0 && h->bins >= 64);
-        const int wpc = pv::std_analysis_wgs_per_cu(h->L_ana, h->hop, ekl, h->packed != 0);
+        int W = 4;
+        const int wpc = pv::std_analysis_wgs_per_cu(h->L_ana, h->hop, ekl, h->packed != 0, &W);
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
             cus > 0 && wpc > 0) {
             const long long slots = (long long)cus * wpc;
             const long long C = std::max(cfg->max_channels, 1), T = std::max(cfg->max_frames, 1);
             long long best = -1;
             for (int f = 48; f <= 96; f += 2) {
-                const long long wgs = C * (((T + f - 1) / f + 3) / 4);
+                const long long wgs = C * (((T + f - 1) / f + W - 1) / W);
                 const long long cost = ((wgs + slots - 1) / slots) * f;
                 if (best < 0 || cost < best) { best = cost; F = f; }
             }

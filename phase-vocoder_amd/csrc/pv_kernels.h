@@ -150,7 +150,7 @@ struct MixParams {
 };
 
 hipError_t launch_std_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
-int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed);
+int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed, int* waves_per_wg);
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
