@@ -88,11 +88,19 @@ def _pvref():
 
 
 def _oracle_batch(pvref, compat):
-    """The oracle's batched path: (x, N, hop_div, effect, scale, frames, threads) ->
-    (out, threads used).  REF_COMPAT: the fp64 restatement of kernel.cu / main.cpp."""
+    """The oracle's batched path (the checker): (x, N, hop_div, effect, scale, frames,
+    threads) -> (out, threads used).  REF_COMPAT: the fp64 restatement of kernel.cu /
+    main.cpp; STANDARD: the fp32-contract analysis + fp64 textbook synthesis."""
     if compat:
         return lambda x, N, hd, e, s, fr, th: pvref.compat_process_batch(x, N, hd, fr, th)
     return pvref.std_process_batch
+
+
+def _port_batch(pvref, compat):
+    """What cpu_baseline times: STANDARD — the fp32 CPU port (oracle/pvport.c: the
+    contract's fp32 analysis, the integer phase scan, fp32 sin/cos, fp32 inverse FFT and
+    overlap-add, OpenMP over channels); REF_COMPAT — the fp64 restatement (no fp32 port)."""
+    return _oracle_batch(pvref, True) if compat else pvref.port_std_process_batch
 
 
 def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, compat=False):
@@ -100,9 +108,9 @@ def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, comp
     the SAME host channels the GPU processes (x: [C, n] float32).  A single stream
     (single=True) has no channel parallelism and runs on one core."""
     pvref = _pvref()
-    batch = _oracle_batch(pvref, compat)
+    batch = _port_batch(pvref, compat)
     what = ("oracle/pvref.c REF_COMPAT fp64 restatement" if compat
-            else "oracle/pvref.c fp32-contract analysis + fp64 synthesis")
+            else "oracle/pvport.c fp32 CPU port")
     threads, aff = cpu_share()
     C_all, n = x.shape
     frames = pvref.num_frames(n, N // hop_div)
@@ -111,7 +119,10 @@ def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, comp
     # reference would be, so the GPU/CPU ratio it gives is overstated (said in the line)
     note = ("fp64 restatement of kernel.cu / main.cpp, not an fp32 port: an fp32 CPU port would "
             "be faster, so the GPU/CPU ratio is overstated" if compat else
-            "fp32-contract analysis (the GPU's own phases) + fp64 synthesis")
+            "fp32 end to end: the fp32-contract analysis (the GPU's own phases), the integer "
+            "phase scan, fp32 sin/cos, fp32 inverse real FFT and overlap-add; gcc -O3 "
+            "-march=x86-64-v3, OpenMP over channels (pinned to the fp64 oracle <= 1e-6 RMS, "
+            "tests/test_oracle.py)")
     if single:
         t0 = time.perf_counter()
         _, used = batch(x[:1], N, hop_div, effect, scale, frames, 1)
@@ -224,7 +235,12 @@ def main():
     cdev = dev if backend == "nccl" else torch.device("cpu")
 
     from pvamd import PITCH_SHIFT, REF_COMPAT, PhaseVocoder, STANDARD, TIME_SHIFT
-    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED
+    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED, diagnostic_build
+    # a diagnostic build (timing-only ablations: wrong outputs) is for --no-check A/B runs only
+    diag = diagnostic_build()
+    if diag and not args.no_check:
+        raise SystemExit("bench.py: libpv is a diagnostic build (PV_DIAGNOSTIC_BUILD): "
+                         "timing-only, run it with --no-check")
 
     wl = "c3" if args.workload == "batch" else args.workload
     # (N, hop_div, effect, scale, seconds, channels per GPU, description)
@@ -387,6 +403,7 @@ def main():
                        "parallelism": f"channel-shard x{world}",
                        "dist_backend": backend if distributed else None},
             "roofline": roof,
+            "diagnostic_build": diag,
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
             "measured_ceiling": ceiling,
             "kernels": kernels,
@@ -418,7 +435,10 @@ def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat):
             "synthesis": 8 * B_read + 4 * hop_s,    # spectrum read + emitted output
             "carry": 0, "runsum": 8 * B, "seam": 0,
             # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
-            "fused": 4 * hop_a + 8 * B + 4 * hop_s}.get(kernel, 0)
+            "fused": 4 * hop_a + 8 * B + 4 * hop_s,
+            # real-time push (pv_rt.hip): the callback's new input and emitted output (§8(d)
+            # fused-mode bytes; the spectrum is not written)
+            "rt": 4 * hop_a + 4 * hop_s}.get(kernel, 0)
 
 
 def alg_flops_per_frame(kernel, N, compat):
@@ -435,7 +455,7 @@ def alg_flops_per_frame(kernel, N, compat):
     ana = 2.5 * N * lg + N + 25 * b
     syn = 2.5 * N * lg + 4 * N + (5 if compat else 15) * b
     return {"analysis": ana, "compat_analysis": 5 * 2 * N * math.log2(2 * N) + N + 5 * b,
-            "synthesis": syn, "fused": ana + syn}.get(kernel, 0.0)
+            "synthesis": syn, "fused": ana + syn, "rt": ana + syn}.get(kernel, 0.0)
 
 
 def kernel_sources_sha():
@@ -449,17 +469,25 @@ def kernel_sources_sha():
     return h.hexdigest()[:16]
 
 
+# a roof "binds" when the kernel reaches this fraction of it; below it on both roofs the
+# kernel is latency-bound at its occupancy (the regime named in `bound`)
+BIND_FRAC = 0.75
+
+
 def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
-             isa_path=os.path.join(ROOT, "profiles", "isa_static.json")):
+             isa_path=os.path.join(ROOT, "profiles", "isa_static.json"),
+             regime_path=os.path.join(ROOT, "profiles", "regime.json")):
     """Both roofs of the dominant kernel ("Report both and state which roof
     binds").  HBM: algorithmic bytes per launch / average launch time against 8 TB/s (the
     metric's "% HBM roofline": `achieved`, `peak`, `frac`).  VALU: algorithmic flops against
     the 157.3 TFLOP/s FP32 peak, and the issue-cycle estimate — the kernel's per-frame loop
     priced at the measured issue cost of each instruction form (scripts/isa_static.py ->
-    profiles/isa_static.json, checked against this build's sources) as a fraction of the
-    SIMD cycles the launch had at the 2.4 GHz peak clock (the chip runs slower under its
-    power cap, so the true busy fraction is higher).  `bound` is the roof with the larger
-    fraction."""
+    profiles/isa_static.json, used only when its source hash matches this build) as a
+    fraction of the SIMD cycles the launch had, at the 2.4 GHz peak clock and at the clock
+    the chip was measured to hold on this workload (profiles/regime.json: the 1400 W cap
+    holds ~1.85 GHz on config 3).  `bound` is "hbm" or "valu" when that roof's fraction
+    exceeds BIND_FRAC, else "latency" — then `latency_evidence` carries the timing-only
+    ablations that place the kernel's time (profiles/regime.json)."""
     t = avg_ms * 1e-3
     alg_bytes = alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat) * frames
     achieved = alg_bytes / t / 1e9
@@ -468,25 +496,49 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
     tflops = fl * frames / t / 1e12
     valu = {"flops_per_frame": fl, "achieved_tflops": tflops, "peak_tflops": VALU_PEAK_TFLOPS,
             "flop_frac": tflops / VALU_PEAK_TFLOPS, "issue_cycles_per_frame": None,
-            "issue_frac_at_peak_clock": None, "issue_source": None}
+            "issue_frac_at_peak_clock": None, "issue_frac_at_measured_clock": None,
+            "measured_clock_ghz": None, "issue_source": None}
+    regime = {}
+    try:
+        regime = json.load(open(regime_path)).get(wl, {})
+    except (OSError, ValueError):
+        regime = {}
     try:
         isa = json.load(open(isa_path))
         ent = isa.get(wl, {}).get(kernel)
         if ent is not None:
-            fresh = isa.get("_sources_sha16") == kernel_sources_sha()
             cyc = ent["valu_cycles_per_frame"]
             valu["issue_cycles_per_frame"] = cyc
-            valu["issue_frac_at_peak_clock"] = cyc * frames / (SIMDS * t * PEAK_SCLK_GHZ * 1e9)
-            valu["issue_source"] = ("profiles/isa_static.json (static count of this build's loop, "
-                                    "measured issue costs)" if fresh else
-                                    "profiles/isa_static.json (STALE: sources changed since)")
+            if isa.get("_sources_sha16") == kernel_sources_sha():
+                valu["issue_frac_at_peak_clock"] = cyc * frames / (SIMDS * t * PEAK_SCLK_GHZ * 1e9)
+                if regime.get("clock_ghz"):
+                    clk = float(regime["clock_ghz"])
+                    valu["measured_clock_ghz"] = clk
+                    valu["clock_source"] = regime.get("clock_source")
+                    valu["issue_frac_at_measured_clock"] = cyc * frames / (SIMDS * t * clk * 1e9)
+                valu["issue_source"] = ("profiles/isa_static.json (static count of this build's loop, "
+                                        "measured issue costs)")
+            else:  # a stale estimate is reported but never used for the regime
+                valu["issue_source"] = "profiles/isa_static.json (STALE: sources changed since; not used)"
     except (OSError, ValueError, KeyError):
         pass
-    vfrac = max(valu["flop_frac"], valu["issue_frac_at_peak_clock"] or 0.0)
-    return {"bound": "valu" if vfrac > hbm_frac else "hbm", "kernel": kernel,
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
-            "frac_of": "hbm (the metric's % HBM roofline)", "traffic": traffic,
-            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms, "valu": valu}
+    issue = valu["issue_frac_at_measured_clock"]
+    if issue is None:
+        issue = valu["issue_frac_at_peak_clock"]
+    vfrac = max(valu["flop_frac"], issue or 0.0)
+    if hbm_frac > BIND_FRAC and hbm_frac >= vfrac:
+        bound = "hbm"
+    elif vfrac > BIND_FRAC:
+        bound = "valu"
+    else:
+        bound = "latency"
+    out = {"bound": bound, "bind_threshold": BIND_FRAC, "kernel": kernel,
+           "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
+           "frac_of": "hbm (the metric's % HBM roofline)", "traffic": traffic,
+           "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms, "valu": valu}
+    if bound == "latency":
+        out["latency_evidence"] = (regime.get(kernel) or {}).get("latency_evidence")
+    return out
 
 
 def bench_rt(args):
@@ -550,6 +602,12 @@ def bench_rt(args):
     k_us = e0.elapsed_time(e1) / 200 * 1e3
     deadline_us = hop / SR * 1e6
     frame_bytes = 4 * hop + 4 * rt.outHopSize  # SURVEY.md §8(d) fused-mode bytes per frame
+    rt_roof = roofline("rt", k_us * 1e-3, "rt", N, hop, rt.outHopSize, N // 2 + 1, C, False, None)
+    assert abs(rt_roof["alg_bytes_per_launch"] - C * frame_bytes) < 1e-6
+    # one callback of 256 frames is ~7 us of device time, mostly launch and dependent latency
+    rt_roof["bound"] = "latency"
+    rt_roof["latency_note"] = ("a callback's kernel moves 256 frames x 512 B: HBM and VALU both idle; "
+                               "the host round trip per callback (latency_us) is what the deadline sees")
     line = {
         "metric": METRIC + " [real-time mode]", "value": C * steps / dt, "unit": "frames/s",
         "n_gpus": 1, "steps": steps, "warmup": warm, "ms_per_step": dt / steps * 1e3,
@@ -564,9 +622,7 @@ def bench_rt(args):
         "kernel_us": k_us,
         "alt_direct_launch": {"value": C * steps / dt_d, "p50_us": float(np.percentile(lat_d, 50)),
                               "p99_us": float(np.percentile(lat_d, 99)), "max_us": float(lat_d.max())},
-        "roofline": {"bound": "latency", "kernel": "rt", "achieved": C * frame_bytes / (k_us * 1e-6) / 1e9,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": C * frame_bytes / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None},
+        "roofline": rt_roof,
         "world_size_env": world,
     }
     print(json.dumps(line), flush=True)

@@ -163,6 +163,9 @@ int pv_abi_version(void);
  * phases and unwrap decisions) this build computes; the CPU oracle states the
  * version it restates (oracle/pvref.h PVR_CONTRACT_VERSION) and the two must agree */
 int pv_contract_version(void);
+/* 1 for a diagnostic build (timing-only ablations or instrumentation compiled in with
+ * PV_DIAGNOSTIC_BUILD: outputs are not the product's), 0 for the product */
+int pv_diagnostic_build(void);
 const char* pv_status_string(pv_status s);
 const char* pv_last_error(void); /* thread-local text of the last failure */
 

@@ -109,7 +109,10 @@ float pvr_atan2f(float y, float x) {
     r0 = fmaf(r0, e2, r0);
     e = fmaf(-mx, r0, 1.0f);
     r0 = fmaf(r0, e, r0);
+    /* contract v4: the ratio clamped to [0, 1], NaN -> 0 (the GPU's clamp modifier with
+     * DX10 clamping): the phase of a non-finite bin is finite, so no decision explodes */
     float a = mn * r0;
+    a = (a >= 0.0f) ? ((a <= 1.0f) ? a : 1.0f) : 0.0f;
     float s = a * a;
     float p = PVR_ATAN_C[9];
     for (int i = 8; i >= 0; --i) p = fmaf(p, s, PVR_ATAN_C[i]);

@@ -29,7 +29,11 @@
  *   1.5*2^23 integer grid) instead of rounding the product and then rintf.  Version 3:
  *   for L = N/2 in [128, 512] the FFT is a Stockham FFT of twiddle-first radix-(L/64) passes
  *   with R-point DIF butterflies (pvr_fft_c32_v3); L >= 1024 keeps the radix-2 Stockham
- *   stages.  The GPU must reproduce these bit-for-bit, because
+ *   stages.  Version 4 (round 5): atan2's ratio is clamped, a = min(max(mn * r, 0), 1)
+ *   with NaN -> 0 (the GPU's clamp output modifier), so every phase is finite: a
+ *   non-finite input sample makes the magnitudes of the frames that contain it NaN, but no
+ *   unwrap decision becomes a huge integer that would shift the channel's output phase for
+ *   the rest of the stream (later frames recover).  The GPU must reproduce these bit-for-bit, because
  *   the phase-unwrap decision (round((dphi - e_k)/2pi)) is discontinuous: any ulp of
  *   difference in a noise bin can flip it and change the output phase by 2*pi*rho.
  *   Everything downstream of the integer decisions is well-conditioned and is computed
@@ -44,7 +48,7 @@
 extern "C" {
 #endif
 
-#define PVR_CONTRACT_VERSION 3
+#define PVR_CONTRACT_VERSION 4
 int pvr_contract_version(void);
 
 typedef struct { float x, y; } pvr_c32;
@@ -113,6 +117,10 @@ void pvr_fft_c64(pvr_c64* data, int L, int inverse);     /* unnormalised radix-2
 int pvr_std_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
                           int effect, float scale, int frames, float* out, long ldo,
                           int threads);
+/* the fp32 CPU port (oracle/pvport.c, bench.py's cpu_baseline): same arguments */
+int pvr_port_std_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
+                               int effect, float scale, int frames, float* out, long ldo,
+                               int threads);
 /* REF_COMPAT (pvr_compat_process, the 4-argument constructor's Hamming) per channel */
 int pvr_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
                              int frames, float* out, long ldo, int threads);

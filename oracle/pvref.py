@@ -72,6 +72,8 @@ def lib():
         L.pvr_std_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                             c_float, c_int, _f32p, c_long, c_int]
         L.pvr_std_process_batch.restype = c_int
+        L.pvr_port_std_process_batch.argtypes = L.pvr_std_process_batch.argtypes
+        L.pvr_port_std_process_batch.restype = c_int
         L.pvr_compat_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                                _f32p, c_long, c_int]
         L.pvr_compat_process_batch.restype = c_int
@@ -243,6 +245,22 @@ def std_process_batch(x, N, hop_div, effect, scale, frames=None, threads=0):
     out = np.zeros((C, olen), np.float32)
     used = lib().pvr_std_process_batch(x, n, n, C, N, hop_div, effect, float(scale), frames,
                                        out, olen, int(threads))
+    return out, used
+
+
+def port_std_process_batch(x, N, hop_div, effect, scale, frames=None, threads=0):
+    """The fp32 CPU port (oracle/pvport.c): x [C, n] float32 -> (out [C, len] float32,
+    threads used).  bench.py's cpu_baseline; pinned to std_process_batch by the tests."""
+    x = _c32(x)
+    C, n = x.shape
+    hop = N // hop_div
+    if frames is None:
+        frames = num_frames(n, hop)
+    hs = out_hop(N, hop_div, effect, scale)
+    olen = frames * hs + (N - hs)
+    out = np.zeros((C, olen), np.float32)
+    used = lib().pvr_port_std_process_batch(x, n, n, C, N, hop_div, effect, float(scale), frames,
+                                            out, olen, int(threads))
     return out, used
 
 

@@ -437,7 +437,14 @@ int pv_abi_version(void) { return PV_ABI_VERSION; }
 
 // 2 (round 4): fused real-split accumulation, one-rounding unwrap decision (pv_device.hpp);
 // 3: twiddle-first radix-E FFT passes with the window folded in, L <= 512 (fft_pass v3)
-int pv_contract_version(void) { return 3; }
+int pv_contract_version(void) { return 4; }
+int pv_diagnostic_build(void) {
+#ifdef PV_DIAGNOSTIC_BUILD
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 const char* pv_status_string(pv_status s) {
     switch (s) {
@@ -595,22 +602,27 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if (h->L_syn >= 1024 && F > 32) F = 32;
     // Large STANDARD batches at L <= 512: the analysis grid runs in rounds of (workgroups one
     // CU holds) x CUs, and a last partial round leaves most of the chip idle while its runs
-    // finish.  Among F = 48 .. 96 take the one with the fewest frame-times, rounds x F (ties:
-    // the shorter runs).  Config 3 (1024 x 1722 frames, 5 workgroups per CU, 256 CUs): 48
-    // gives 9216 workgroups = 8 rounds (the last a fifth full) x 48 = 384, 88 gives 5120 = 4
-    // x 88 = 352 (measured on two boxes: +1.7 / +1.8 % frames/s, profiles/r04_ab_c3_F.txt).
+    // finish.  Among F = 48, 56, .. 96 take the one with the fewest frame-times, rounds x F
+    // (ties: the shorter runs).  Config 3 (1024 x 1722 frames, 5 workgroups per CU): 48 gives
+    // 9216 workgroups = 8 rounds (the last a fifth full) x 48 = 384, 88 gives 5120 = 4 x 88 =
+    // 352 (measured on two boxes: +1.7 / +1.8 % frames/s, profiles/r04_ab_c3_F.txt; what the
+    // longer runs buy is the carry, seam and synthesis time — the analysis kernel itself is
+    // within +-2 % from F = 24 to 88, profiles/r05_ab_c3_F_sweep.txt).  The rounds are counted
+    // on the MI355X's 256 CUs whatever device the handle is on, and the workgroups per CU
+    // come from the compiled kernel's resources: F, which sets where the overlap-add sums are
+    // split into run seams (their rounding, <= 1e-6), depends only on the configuration, so
+    // the same batch gives the same output bits on any gfx950 device or partition mode.
     if (F == 48 && h->L_ana <= 512 && h->mode == PV_MODE_STANDARD) {
         DeviceGuard g0(cfg->device);
-        int cus = 0;
+        constexpr int kRoundCUs = 256;  // MI355X
         const bool ekl = (64 % cfg->hop_div == 0 && h->bins >= 64);
         int W = 4;
         const int wpc = pv::std_analysis_wgs_per_cu(h->L_ana, h->hop, ekl, h->packed != 0, &W);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
-            cus > 0 && wpc > 0) {
-            const long long slots = (long long)cus * wpc;
+        if (wpc > 0) {
+            const long long slots = (long long)kRoundCUs * wpc;
             const long long C = std::max(cfg->max_channels, 1), T = std::max(cfg->max_frames, 1);
             long long best = -1;
-            for (int f = 48; f <= 96; f += 2) {
+            for (int f = 48; f <= 96; f += 8) {
                 const long long wgs = C * (((T + f - 1) / f + W - 1) / W);
                 const long long cost = ((wgs + slots - 1) / slots) * f;
                 if (best < 0 || cost < best) { best = cost; F = f; }

@@ -249,7 +249,11 @@ __device__ __forceinline__ float atan2_pv(float y, float x) {
     r = __builtin_fmaf(r, e2, r);
     e = __builtin_fmaf(-mx, r, 1.0f);
     r = __builtin_fmaf(r, e, r);
-    float a = mn * r;
+    // contract v4: a = clamp(mn r, 0, 1) by the output modifier (DX10 clamp: NaN -> 0, the
+    // kernels' default mode), so the phase is finite for any input: no unwrap decision of a
+    // non-finite bin corrupts the channel's run sums
+    float a;
+    asm("v_mul_f32_e64 %0, %1, %2 clamp" : "=v"(a) : "v"(mn), "v"(r));
     float s = a * a;
     float p = -0x1.8ba68ap-10f;
     p = __builtin_fmaf(p, s, 0x1.398008p-7f);
@@ -288,7 +292,8 @@ __device__ __forceinline__ f2v atan2_pv2(float y0, float x0, float y1, float x1)
     r = __builtin_elementwise_fma(r, e2, r);
     e = __builtin_elementwise_fma(-mx, r, one);
     r = __builtin_elementwise_fma(r, e, r);
-    const f2v a = mn * r;
+    f2v a;  // contract v4: clamp(mn r, 0, 1), NaN -> 0 (atan2_pv)
+    asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(a) : "v"(mn), "v"(r));
     const f2v sq = a * a;
     auto c = [](float v) { return f2v{v, v}; };
     f2v p = c(-0x1.8ba68ap-10f);

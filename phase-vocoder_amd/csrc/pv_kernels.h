@@ -3,6 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+// Diagnostic builds.  The timing-only ablation switches (PV_ABL_*) give WRONG outputs and
+// PV_FUSED_STAMPS writes per-wave clock stamps; a build that defines one must say so with
+// PV_DIAGNOSTIC_BUILD, and the library then reports it (pv_diagnostic_build() = 1): bench.py
+// refuses to check or report such a build as the product, and the GPU tests refuse it.
+#if (defined(PV_ABL_NOSTORE) || defined(PV_ABL_NOATAN) || defined(PV_ABL_NOFFT) || defined(PV_ABL_NOWIN) ||   \
+     defined(PV_ABL_L2IN) || defined(PV_ABL_L2ROWS) || defined(PV_ABL_NOSINCOS) || defined(PV_ABL_NOGATHER) || \
+     defined(PV_FUSED_STAMPS)) &&                                                                            \
+    !defined(PV_DIAGNOSTIC_BUILD)
+#error "diagnostic / timing-only switch without PV_DIAGNOSTIC_BUILD (its outputs are wrong or instrumented)"
+#endif
+
 namespace pv {
 
 // STANDARD run record per (channel, run): kRecFields rows of bins_pad int32 words —

@@ -78,6 +78,8 @@ def lib():
     L.pv_abi_version.restype = i
     if hasattr(L, "pv_contract_version"):  # (A/B builds of older revisions lack it)
         L.pv_contract_version.restype = i
+    if hasattr(L, "pv_diagnostic_build"):
+        L.pv_diagnostic_build.restype = i
     L.pv_status_string.argtypes = [i]
     L.pv_status_string.restype = ctypes.c_char_p
     L.pv_last_error.restype = ctypes.c_char_p
@@ -150,3 +152,10 @@ def check(status: int, what: str = "pv call"):
 
 def frame_count(n_samples: int, hop: int) -> int:
     return lib().pv_frame_count(int(n_samples), int(hop))
+
+
+def diagnostic_build() -> bool:
+    """True when the loaded libpv was built with PV_DIAGNOSTIC_BUILD (timing-only ablations
+    or instrumentation: not the product)."""
+    L = lib()
+    return bool(L.pv_diagnostic_build()) if hasattr(L, "pv_diagnostic_build") else False

@@ -3,7 +3,7 @@
 stamps s_memrealtime (100 MHz) at its start, after the table set-up barrier, after each of
 its F frames, after the frame loop and at its end, in a diagnostic build only
 
-  make -C phase-vocoder_amd/csrc -j8 variant NAME=stamps DEFS=-DPV_FUSED_STAMPS
+  make -C phase-vocoder_amd/csrc -j8 variant NAME=stamps DEFS="-DPV_FUSED_STAMPS -DPV_DIAGNOSTIC_BUILD"
   PV_LIB_PATH=phase-vocoder_amd/build/variants/libpv_stamps.so python scripts/fused_stamps.py
 
 (the product kernel executes no stamp).  Runs config 2 (one 60 s stream, N = 1024, pitch

@@ -34,6 +34,11 @@ KERNELS = {
     ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
+    # config 2's single launch: analysis + synthesis of a frame in one loop trip (9 + 17)
+    ("c2", "fused"): ("pv_fused.hip", [], "_ZN2pv7k_fusedILi512ELi3ELi2EE", 26),
+    # config 5's per-callback kernel: one frame per wave and launch, no frame loop — the whole
+    # kernel is priced (table staging included, its loops counted once); L = 128: 3 + 5
+    ("rt", "rt"): ("pv_rt.hip", [], "_ZN2pv4k_rtILi128ELi2ELb1EE", None),
 }
 
 # issue cycles per wave-instruction at 8 waves/SIMD (measured; see the module docstring)
@@ -115,11 +120,13 @@ def price(seg, extra):
 
 
 def frame_loop(asm, prefix, trans_pf, extra):
-    """The steady-state frame loop: among the innermost loops that hold a frame's work (LDS
-    permutes and global stores), the one with the fewest VALU cycles per frame (the path every
+    """The steady-state frame loop: among the innermost loops that hold a frame's work (its
+    square roots / sines / cosines and global stores), the one with the fewest VALU cycles per frame (the path every
     full run takes; the bounds-checked variants for the channel ends cost more)."""
+    def trans(seg):
+        return sum(1 for o, _ in seg if o.startswith(("v_sin", "v_cos", "v_sqrt")))
     cands = [(a, b, seg) for a, b, seg in loops_of(asm, prefix)
-             if any(o.startswith("ds_bpermute") for o, _ in seg) and any(o.startswith("global_store") for o, _ in seg)]
+             if trans(seg) >= trans_pf and any(o.startswith("global_store") for o, _ in seg)]
     inner = [c for c in cands if not any(o is not c and c[0] <= o[0] and o[1] <= c[1] for o in cands)]
     best = None
     for a, b, seg in inner:
@@ -149,6 +156,15 @@ def main():
                 subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *fl, "-o", asm, os.path.join(CSRC, src)],
                                check=True, stderr=subprocess.DEVNULL)
                 cache[(src, tuple(fl))] = asm
+            if trans_pf is None:  # no frame loop: the whole kernel is one frame
+                seg = [(ln.strip().split()[0], ln.strip()) for ln in function_body(asm, prefix)
+                       if ln.strip() and not ln.strip().startswith((";", ".")) and not ln.endswith(":")]
+                cnt, cyc = price(seg, extra)
+                out.setdefault(wl, {})[key] = {"symbol": prefix, "kernel_instructions": len(seg),
+                                               "frames_per_trip": 1, "scope": "whole kernel (loops counted once)",
+                                               "counts_per_trip": dict(cnt),
+                                               "valu_cycles_per_frame": round(cyc, 1)}
+                continue
             best = frame_loop(asm, prefix, trans_pf, extra)
             if best is None:
                 continue

@@ -29,4 +29,8 @@ def cuda():
     if not gpu_available():
         pytest.skip("no GPU")
     import torch
+    from pvamd import _lib
+    # the GPU tests check the product: a diagnostic build (timing-only ablations,
+    # instrumentation; pv_diagnostic_build() = 1) is refused loudly
+    assert not _lib.diagnostic_build(), f"{_lib.LIB_PATH} is a diagnostic build (PV_DIAGNOSTIC_BUILD)"
     return torch.device("cuda:0")

@@ -41,7 +41,7 @@ def test_contract_version_matches_oracle():
     (DESIGN.md §3.2): a library and an oracle of different versions would disagree in the
     last bits of the phases and hence in unwrap decisions."""
     import pvref
-    assert _lib.lib().pv_contract_version() == pvref.contract_version() == 3
+    assert _lib.lib().pv_contract_version() == pvref.contract_version() == 4
 
 
 def test_frame_count_is_main_cpp_loop():
@@ -157,17 +157,27 @@ def test_static_inline_helpers_are_not_abi_symbols():
 
 
 def test_fused_stamps_diagnostic_compiles():
-    """The one diagnostic build configuration left in the sources (PV_FUSED_STAMPS: per-wave
-    phase stamps of the config-2 single launch, scripts/fused_stamps.py) still compiles."""
+    """The diagnostic build configurations (PV_FUSED_STAMPS: per-wave phase stamps of the
+    config-2 single launch, scripts/fused_stamps.py; the PV_ABL_* timing-only ablations)
+    compile only together with PV_DIAGNOSTIC_BUILD, which the library then reports."""
     import subprocess
     csrc = os.path.join(_lib.ROOT, "phase-vocoder_amd", "csrc")
     for src in ("pv_fused.hip", "pv_api.cpp"):
         cmd = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-               "-DPV_FUSED_STAMPS", "-fPIC", "-c", os.path.join(csrc, src), "-o", os.devnull]
+               "-DPV_FUSED_STAMPS", "-DPV_DIAGNOSTIC_BUILD", "-fPIC", "-c", os.path.join(csrc, src), "-o", os.devnull]
         if src.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-2000:]
+    # without PV_DIAGNOSTIC_BUILD an ablation switch is a compile error
+    cmd = ["/opt/rocm/bin/hipcc", "-x", "hip", "-O0", "-std=c++17", "--offload-arch=gfx950", "-DPV_ABL_NOSTORE",
+           "-fsyntax-only", os.path.join(csrc, "pv_api.cpp")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0 and "PV_DIAGNOSTIC_BUILD" in r.stderr
+
+
+def test_product_library_is_not_diagnostic():
+    assert _lib.diagnostic_build() is False
 
 
 def test_device_asm_has_no_prefetch_or_scc_hazards(tmp_path):

@@ -84,10 +84,15 @@ def test_compat_oracle_batch_and_baseline():
 
 def test_roofline_reports_both_roofs(tmp_path):
     """the line carries the HBM and the VALU roof of the dominant kernel and
-    names the binding one (`bound`: the larger fraction)."""
+    names the regime: "hbm" / "valu" when that roof's fraction exceeds bench.BIND_FRAC,
+    otherwise "latency" with the ablation evidence of profiles/regime.json."""
     import json
     N, hop, hs, B, frames = 1024, 256, 128, 512, 1024 * 1722
-    r = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None)
+    regime = tmp_path / "regime.json"
+    regime.write_text(json.dumps({"c3": {"clock_ghz": 1.85, "clock_source": "test",
+                                         "analysis": {"latency_evidence": {"memory_side_ms": 1.86}}}}))
+    kw = dict(regime_path=str(regime))
+    r = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, **kw)
     assert r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["achieved"] - (4 * hop + 8 * B) * frames / 2e-3 / 1e9) < 1e-6
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12
@@ -99,19 +104,47 @@ def test_roofline_reports_both_roofs(tmp_path):
     assert abs(tot - (5 * N * 10 + 5 * N + 40 * 513)) < 1e-9 and 76e3 < tot < 78e3
     comp = bench.alg_flops_per_frame("compat_analysis", N, True) + bench.alg_flops_per_frame("synthesis", N, True)
     assert 147e3 < comp < 150e3
-    assert r["bound"] in ("hbm", "valu")
-    # the issue estimate from a static-count file, and `bound` follows the larger fraction
-    isa = tmp_path / "isa.json"
-    isa.write_text(json.dumps({"_sources_sha16": bench.kernel_sources_sha(),
-                               "c3": {"analysis": {"valu_cycles_per_frame": 4000.0}}}))
-    r2 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=str(isa))
-    f = 4000.0 * frames / (1024 * 2e-3 * 2.4e9)
+    assert r["bound"] in ("hbm", "valu", "latency")
+
+    def isa_file(sha, cyc):
+        p = tmp_path / "isa.json"
+        p.write_text(json.dumps({"_sources_sha16": sha, "c3": {"analysis": {"valu_cycles_per_frame": cyc}}}))
+        return str(p)
+
+    sha = bench.kernel_sources_sha()
+    # issue fractions at the peak and at the measured clock
+    r2 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file(sha, 1600.0), **kw)
+    f = 1600.0 * frames / (1024 * 2e-3 * 2.4e9)
     assert abs(r2["valu"]["issue_frac_at_peak_clock"] - f) < 1e-12
-    assert r2["bound"] == ("valu" if f > r2["frac"] else "hbm")
+    fm = 1600.0 * frames / (1024 * 2e-3 * 1.85e9)
+    assert abs(r2["valu"]["issue_frac_at_measured_clock"] - fm) < 1e-12
+    assert r2["valu"]["measured_clock_ghz"] == 1.85
     assert "STALE" not in r2["valu"]["issue_source"]
-    isa.write_text(json.dumps({"_sources_sha16": "0", "c3": {"analysis": {"valu_cycles_per_frame": 1.0}}}))
-    r3 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=str(isa))
-    assert "STALE" in r3["valu"]["issue_source"] and r3["bound"] == "hbm"
+    # HBM 0.56, issue 0.73 at the measured clock: neither roof binds -> latency, with evidence
+    assert r2["frac"] < bench.BIND_FRAC and fm < bench.BIND_FRAC
+    assert r2["bound"] == "latency" and r2["latency_evidence"] == {"memory_side_ms": 1.86}
+    # an issue fraction above the threshold binds
+    r3 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file(sha, 2400.0), **kw)
+    assert r3["bound"] == "valu" and "latency_evidence" not in r3
+    # so does the HBM roof
+    r4 = bench.roofline("analysis", 1.2, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file(sha, 100.0), **kw)
+    assert r4["frac"] > bench.BIND_FRAC and r4["bound"] == "hbm"
+    # a stale estimate is reported but never decides the regime
+    r5 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file("0", 4000.0), **kw)
+    assert "STALE" in r5["valu"]["issue_source"] and r5["valu"]["issue_frac_at_peak_clock"] is None
+    assert r5["bound"] == "latency"
+
+
+def test_committed_regime_evidence():
+    """profiles/regime.json carries the measured clock and the latency evidence of the
+    headline kernel, citing its sources."""
+    import json
+    reg = json.load(open(os.path.join(ROOT, "profiles", "regime.json")))
+    ev = reg["c3"]["analysis"]["latency_evidence"]
+    assert 1.5 < reg["c3"]["clock_ghz"] < 2.4 and "r04_clock_power_c3" in reg["c3"]["clock_source"]
+    assert ev["memory_side_ms"] > 0 and "r04_ab_c3_ablation" in ev["sources"]
+    for src in ("r04_ab_c3_ablation.txt", "r05_mix_probe.jsonl", "r05_ab_ring.json"):
+        assert os.path.exists(os.path.join(ROOT, "profiles", src))
 
 
 def test_committed_isa_static_matches_sources():
@@ -120,5 +153,6 @@ def test_committed_isa_static_matches_sources():
     import json
     isa = json.load(open(os.path.join(ROOT, "profiles", "isa_static.json")))
     assert isa["_sources_sha16"] == bench.kernel_sources_sha()
-    for wl, k in (("c3", "analysis"), ("c3", "synthesis"), ("c4", "synthesis"), ("compat", "compat_analysis")):
+    for wl, k in (("c3", "analysis"), ("c3", "synthesis"), ("c4", "analysis"), ("c4", "synthesis"),
+                  ("compat", "compat_analysis"), ("c2", "fused"), ("rt", "rt")):
         assert isa[wl][k]["valu_cycles_per_frame"] > 0

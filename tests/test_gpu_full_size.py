@@ -2,14 +2,16 @@
 cannot redo a 1.7-million-frame batch in a test): the per-GPU workloads of configs 2, 3 and
 4 run whole, and
 
-* every output sample is finite and the output has pv_output_length samples;
+* every output sample is finite and the output has exactly pv_output_length samples, the
+  length the oracle's output has too (no truncation before the comparison);
 * a channel's result does not depend on the batch it is in: channels run alone, and the
   upper half of the channels run as their own batch (what one rank of the multi-GPU shard
   does), equal the full batch bit for bit at the same run length (PV_RUN_FRAMES: the run
   length sets where the overlap-add sums are split into run seams, so it sets their
   rounding);
 * a second run is bit-identical (no atomics, no order-dependent reductions);
-* the first and the last channel match the CPU oracle within the north_star tolerance;
+* 16 channels spread over the batch (first and last included, bench.py's check_channels)
+  match the CPU oracle within the north_star tolerance;
 * spectrum magnitudes are >= 0 and phases lie in [-pi, pi]."""
 import os
 import sys
@@ -23,7 +25,7 @@ from pvamd import _lib
 from test_gpu_parity import RMS_TOL, rms
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import cpu_share, synth_channels_np  # noqa: E402
+from bench import check_channels, cpu_share, synth_channels_np  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -50,8 +52,10 @@ def test_full_size_properties(cuda, monkeypatch, wl):
     pv.process(x, spec=spec, out=out)
     torch.cuda.synchronize()
     olen = pv.output_length(fr)
-    assert out.shape[-1] >= olen
-    full = out[:, :olen]
+    hs = pv.outHopSize
+    assert olen == fr * hs + (N - hs)         # the full overlap-add length (pv.h pv_output_length)
+    assert out.shape == (C, olen)
+    full = out
     assert bool(torch.isfinite(full).all())
     ref_bits = full.cpu().numpy().view(np.uint32).copy()
 
@@ -80,10 +84,10 @@ def test_full_size_properties(cuda, monkeypatch, wl):
         oh, _ = half.process(x[h:].contiguous())
         assert np.array_equal(oh[:, :olen].cpu().numpy().view(np.uint32), ref_bits[h:])
 
-    # the oracle on the first and the last channel
-    idx = sorted({0, C - 1})
-    ref, _ = pvref.std_process_batch(x_host[idx], N, 4, ord(effect), scale)
+    # the oracle on 16 channels spread over the batch, whole rows (same length, no truncation)
+    idx = check_channels(C)
+    ref, _ = pvref.std_process_batch(x_host[idx], N, 4, ord(effect), scale, fr, cpu_share()[0])
     g = full[idx].cpu().numpy()
-    for j in range(len(idx)):
-        m = min(ref.shape[1], g.shape[1])
-        assert rms(g[j, :m], ref[j, :m]) <= RMS_TOL
+    assert ref.shape == g.shape == (len(idx), olen)
+    for j, c in enumerate(idx):
+        assert rms(g[j], ref[j]) <= RMS_TOL, f"channel {c}"

@@ -241,11 +241,13 @@ def test_odd_output_stride(cuda, mode):
     assert torch.all(big[:, olen:] == 7.0)  # nothing written past the row
 
 
-@pytest.mark.parametrize("F", [8, 16, 32, 48, 64])
+@pytest.mark.parametrize("F", [8, 16, 32, 42, 48, 64, 72, 88])
 @pytest.mark.parametrize("effect,scale", [(TIME_SHIFT, 0.5), (PITCH_SHIFT, 1.5)])
 def test_run_length_geometries(cuda, monkeypatch, F, effect, scale):
-    """Every frames-per-run the handle may pick (F = 48 for config-3-sized batches) gives
-    the oracle's output; run boundaries only move the seams (<= 1e-6 between runs)."""
+    """Run lengths the handle can pick (8, 16, 32 for small batches; a multiple of 8 in
+    48 .. 96 for large ones at L <= 512 — 88 for config 3) and any even PV_RUN_FRAMES override
+    (42: F = 2 mod 4) give the oracle's output; run boundaries only move the seams
+    (<= 1e-6 between runs)."""
     N, hop_div, C = 1024, 4, 3
     xs = np.stack([synth(110250, 20240 + c) for c in range(C)])
     monkeypatch.setenv("PV_RUN_FRAMES", str(F))
@@ -285,3 +287,36 @@ def test_short_input_between_n_minus_hop_and_n(cuda, n):
     one = PhaseVocoder(N, TIME_SHIFT, 0.5, hop_div, mode=STANDARD, max_frames=8)
     o1, _ = one.process(buf[:n])
     assert torch.equal(o1[0], out[0])
+
+
+@pytest.mark.parametrize("effect,scale", [(TIME_SHIFT, 0.5), (PITCH_SHIFT, 1.5)])
+def test_nonfinite_burst_recovers(cuda, effect, scale):
+    """Contract v4: a burst of NaN and Inf input samples makes the frames that contain it
+    non-finite, but every phase stays finite (atan2's clamped ratio), so no unwrap decision
+    corrupts the run sums and carries: the output after the burst's last frame is finite and
+    matches the oracle (which restates the same clamp), and the phases are bit-exact."""
+    N, hop_div = 1024, 4
+    hop = N // hop_div
+    x = synth(60000, 99)
+    x[20000:20010] = np.nan
+    x[20100] = np.inf
+    x[20200] = -np.inf
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_frames=400)
+    out, spec = pv.process(to_dev(x))
+    frames = pv.num_frames(len(x))
+    _, ph = pvref.std_analysis(x, N, hop, frames)
+    g_ph = spec[0, :frames, :N // 2 + 1, 1].cpu().numpy()
+    assert np.all(np.isfinite(g_ph)) and np.all(np.isfinite(ph))
+    assert np.array_equal(g_ph.view(np.uint32), ph.view(np.uint32))
+    g = out.cpu().numpy()[0]
+    ref = pvref.std_process(x, N, hop_div, ord(effect), scale)
+    assert g.shape == ref.shape
+    # output samples of frames that start after the burst's last sample
+    last_bad = (20200 // hop) + 1
+    hs = pv.outHopSize
+    start = (last_bad + 1) * hs + N
+    assert np.all(np.isfinite(g[start:])) and np.all(np.isfinite(ref[start:]))
+    assert rms(g[start:], ref[start:]) <= RMS_TOL
+    # and before the burst too
+    first_bad = 20000 // hop - N // hop
+    assert rms(g[:max(first_bad, 0) * hs], ref[:max(first_bad, 0) * hs]) <= RMS_TOL

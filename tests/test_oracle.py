@@ -331,3 +331,18 @@ def test_compat_nan_faithful_poisons_only_silent_frames_span():
     assert np.array_equal(np.nonzero(nan)[0], np.arange(0, (len(silent) - 1) * hop + N))
     y0 = pvref.compat_process(x, N, hd)
     assert np.all(np.isfinite(y0)) and np.array_equal(y0[~nan], y[~nan])
+
+
+@pytest.mark.parametrize("N,effect,scale", [(1024, "t", 0.5), (1024, "p", 1.5), (1024, "p", 2.0),
+                                            (2048, "p", 1.5), (1024, "t", 1.5), (1024, "p", 0.75),
+                                            (512, "t", 1.0)])
+def test_fp32_port_pinned_to_oracle(N, effect, scale):
+    """The fp32 CPU port bench.py times as cpu_baseline (oracle/pvport.c) computes the same
+    output as the fp64 checker: <= 1e-6 RMS per sample on every channel."""
+    import bench
+    x = bench.synth_channels_np(3, 44100 * 2, 20240)
+    ref, _ = pvref.std_process_batch(x, N, 4, ord(effect), scale, None, 2)
+    got, used = pvref.port_std_process_batch(x, N, 4, ord(effect), scale, None, 2)
+    assert got.shape == ref.shape and used >= 1
+    err = np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2, axis=1))
+    assert err.max() <= 1e-6, err
