@@ -88,11 +88,12 @@ void pvr_expected_advance(int N, int hop, float* e, int* j) {
 
 float pvr_atan2f(float y, float x) {
     float ax = fabsf(x), ay = fabsf(y);
-    float mx = (ax > ay) ? ax : ay;
-    float mn = (ax > ay) ? ay : ax;
-    /* mx floored at FLT_MIN: an all-zero bin gets a = 0 and the phase +-0 (the sign of
-     * y), without a special case */
-    if (mx < 0x1p-126f) mx = 0x1p-126f;
+    /* IEEE maxNum / minNum (a NaN operand yields the other), as the GPU's v_max3_f32 /
+     * v_min_f32 in IEEE mode; mx floored at FLT_MIN: an all-zero bin gets a = 0 and the
+     * phase +-0 (the sign of y), without a special case.  (Contract v4: a bin whose
+     * components are both NaN — a frame with a non-finite sample — gets a = 0, phase +-0.) */
+    float mx = fmaxf(fmaxf(ax, ay), 0x1p-126f);
+    float mn = fminf(ax, ay);
     /* a = mn / mx without a division: reciprocal of mx from an integer seed (relative
      * error <= 5.1e-2), a cubic and a Newton step (below), then one product; <= 6e-8
      * relative for normal mx (audio spectra are far from the fp32 range ends).  The GPU
