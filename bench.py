@@ -182,6 +182,9 @@ def main():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the timed batch (profiling passes only)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--write-spec", action="store_true",
+                    help="c2 (single launch): also write the spectrum rows to HBM (by default the "
+                         "fused path keeps them on chip: SURVEY §8(d) fused mode)")
     ap.add_argument("--layout", choices=["packed", "natural"], default="packed",
                     help="STANDARD spectrum rows of the pv_process workspace (include/pv.h "
                          "pv_spec_layout): packed (default) folds the real bin N/2 into slot 0 "
@@ -276,7 +279,10 @@ def main():
     x_host = synth_channels_np(C, n, 20240 + rank * C, threads)
     x = torch.from_numpy(x_host).to(dev)
     t_gen = time.perf_counter() - t_gen
-    spec = pv.alloc_spec(C, frames)
+    # the single launch (config 2) consumes the spectrum on chip unless --write-spec; the split
+    # path materialises it between its launches (the reference's caller-owned buffers)
+    spec_on_chip = bool(pv.single_launch) and not args.write_spec
+    spec = None if spec_on_chip else pv.alloc_spec(C, frames)
     out = pv.alloc_out(C, frames)
     stream = torch.cuda.current_stream(dev)
 
@@ -285,7 +291,7 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        pv.process(x, spec=spec, out=out)
+        pv.process(x, spec=spec, out=out, spectrum=not spec_on_chip)
     torch.cuda.synchronize(dev)
 
     # kernel durations for the roofline, on the launch stream (pv launches on torch's current
@@ -306,7 +312,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        pv.process(x, spec=spec, out=out)
+        pv.process(x, spec=spec, out=out, spectrum=not spec_on_chip)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
@@ -338,7 +344,8 @@ def main():
                 traffic = ent.get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
-    roof = roofline(dom, avg_ms, wl, N, hop_a, hop_s, B, C * frames, compat, traffic)
+    roof = roofline(dom, avg_ms, wl, N, hop_a, hop_s, B, C * frames, compat, traffic,
+                    spec_written=not spec_on_chip)
     achieved = roof["achieved"]
     # the box's measured HBM ceilings: plain streams (scripts/bw_probe.hip ->
     # profiles/r02_bw_probe.jsonl: copy ~6.0, write ~6.0 TB/s against the 8 TB/s spec) and the
@@ -400,6 +407,8 @@ def main():
             "config": {"workload": wl_desc,
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
                        "out_hop": hop_s, "spec_layout": args.layout,
+                       "spectrum": "kept on chip (single launch, SURVEY §8(d) fused mode)" if spec_on_chip
+                                   else "written to HBM",
                        "parallelism": f"channel-shard x{world}",
                        "dist_backend": backend if distributed else None},
             "roofline": roof,
@@ -424,7 +433,7 @@ SIMDS = 1024               # 256 CUs x 4 SIMDs
 PEAK_SCLK_GHZ = 2.4
 
 
-def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat):
+def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat, spec_written=True):
     """SURVEY §8(d) bytes per frame of each kernel: spectrum row = what the layout stores
     (8 (N/2+1) natural, 8 N/2 packed: bin N/2 rides in slot 0, the smaller figure);
     REF_COMPAT writes 2N bins per frame (kernel.cu:337) and its resynthesis reads the N/2+1
@@ -435,7 +444,8 @@ def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat):
             "synthesis": 8 * B_read + 4 * hop_s,    # spectrum read + emitted output
             "carry": 0, "runsum": 8 * B, "seam": 0,
             # q = 1 single launch (pv_fused.hip): spectrum written once, never re-read
-            "fused": 4 * hop_a + 8 * B + 4 * hop_s,
+            # (spec_written=False: the rows stay on chip, SURVEY's fused-mode bytes)
+            "fused": 4 * hop_a + (8 * B if spec_written else 0) + 4 * hop_s,
             # real-time push (pv_rt.hip): the callback's new input and emitted output (§8(d)
             # fused-mode bytes; the spectrum is not written)
             "rt": 4 * hop_a + 4 * hop_s}.get(kernel, 0)
@@ -476,7 +486,7 @@ BIND_FRAC = 0.75
 
 def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
              isa_path=os.path.join(ROOT, "profiles", "isa_static.json"),
-             regime_path=os.path.join(ROOT, "profiles", "regime.json")):
+             regime_path=os.path.join(ROOT, "profiles", "regime.json"), spec_written=True):
     """Both roofs of the dominant kernel ("Report both and state which roof
     binds").  HBM: algorithmic bytes per launch / average launch time against 8 TB/s (the
     metric's "% HBM roofline": `achieved`, `peak`, `frac`).  VALU: algorithmic flops against
@@ -489,7 +499,7 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
     exceeds BIND_FRAC, else "latency" — then `latency_evidence` carries the timing-only
     ablations that place the kernel's time (profiles/regime.json)."""
     t = avg_ms * 1e-3
-    alg_bytes = alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat) * frames
+    alg_bytes = alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat, spec_written) * frames
     achieved = alg_bytes / t / 1e9
     hbm_frac = achieved / HBM_PEAK_GBS
     fl = alg_flops_per_frame(kernel, N, compat)

@@ -192,7 +192,10 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
                          int frames, const float* ola_in, long long ld_ola, float* out,
                          long long ldo, void* stream);
 
-/* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer). */
+/* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer).  When the
+ * handle takes the single launch (pv_info.single_launch = 1), spec may be NULL: the spectrum
+ * is then computed and consumed on chip and not written (SURVEY §8(d) fused mode); the split
+ * path needs it (PV_ERR_ARG otherwise). */
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);

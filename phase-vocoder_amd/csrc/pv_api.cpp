@@ -386,8 +386,9 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
 pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int C, int frames,
                    pv_float2* spec, long long ld_spec, float* out, long long ldo, hipStream_t s) {
     if (C == 0 || frames == 0) return PV_OK;
-    if (!x || !spec || !out) return fail(PV_ERR_ARG, "null x/spec/out");
-    if (ld_spec < (long long)frames * h->spec_stride)
+    if (!x || !out) return fail(PV_ERR_ARG, "null x/out");
+    // spec == NULL: no spectrum output (the single launch keeps the rows on chip)
+    if (spec && ld_spec < (long long)frames * h->spec_stride)
         return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
     if (C > 1 && ldx < n) return fail(PV_ERR_ARG, "ldx < n_samples");
     const long long olen = pv_output_length(h, frames);
@@ -818,6 +819,8 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     ProfCall pc_(h);
     hipStream_t s = (hipStream_t)stream;
     if (h->F_fused > 0) return do_fused(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
+    if (!spec && channels > 0 && frames > 0)
+        return fail(PV_ERR_ARG, "null spec: the split path's spectrum buffer (only the single launch runs without one)");
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
     if (st != PV_OK) return st;

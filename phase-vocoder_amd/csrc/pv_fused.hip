@@ -89,7 +89,10 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
     const int TL = N - hs;
     float2* tile = tiles + w * G_::TILE;
     const float* xc = p.x + (long long)c * p.ldx;
-    float2* specc = p.spec + (long long)c * p.ld_spec;
+    // spec == nullptr (pv_process without a spectrum buffer): the rows stay in registers
+    // only — SURVEY §8(d)'s fused mode, whose bytes are the input and the output
+    const bool wspec = p.spec != nullptr;
+    float2* specc = wspec ? p.spec + (long long)c * p.ld_spec : nullptr;
     float* outc = p.out + (long long)c * p.ldo;
     const long long obase = (long long)t0 * hs;
 
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                 float magL, phL;
                 bin_l_real_tile<L, true>(tile, twsl, magL, phL);
                 sv[E] = make_float2(magL, phL);
-                if (!p.packed) __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
+                if (wspec && !p.packed) __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
             }
             // bins 0 .. E-1 in pairs: the phases of a pair through the packed-fp32 atan2
             // (atan2_pv2, bit-identical to atan2_pv per half)
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                         mag *= 0.5f;  // X came out doubled (split_chunk TWICE)
                         sv[i] = make_float2(mag, ph);
                         // bins 0..63 go out below (slot 0)
-                        if (i > 0) __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
+                        if (wspec && i > 0) __builtin_nontemporal_store(f2v{mag, ph}, reinterpret_cast<f2v*>(&srow[64 * i]));
                     }
                 });
             });
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
                 const bool pk0 = p.packed && lane == 0;
                 const f2v s0 = pk0 ? f2v{pack_real_bin(sv[0].x, sv[0].y), pack_real_bin(sv[E].x, sv[E].y)}
                                    : f2v{sv[0].x, sv[0].y};
-                __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+                if (wspec) __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
             }
             wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers
@@ -254,11 +257,20 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
         // those go out write-through for the seam hand-off below
         const long long pb = obase + (long long)u * hs + 2 * lane;
         const bool head = (w == 0) && (blockIdx.x > 0) && (u * hs < TL);
+        // the head positions of waves 1..3 are read back by close_seams_inline (intra-workgroup
+        // seam): temporal stores keep them in L2 for that read (non-temporal ones stream past
+        // it and the read-back waits for HBM)
+#ifdef PV_FUSED_NT_HEAD
+        const bool keep = false;
+#else
+        const bool keep = (w > 0) && (u * hs < TL);
+#endif
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const long long gp = pb + 128 * d;
             if (p.out_aligned && gp + 1 < p.out_len) {
                 if (head) st_sc1(outc + gp, f2v{acc[d].x, acc[d].y});
+                else if (keep) *reinterpret_cast<f2v*>(outc + gp) = f2v{acc[d].x, acc[d].y};
                 else __builtin_nontemporal_store(f2v{acc[d].x, acc[d].y}, reinterpret_cast<f2v*>(outc + gp));
             } else if (head) {
                 if (gp < p.out_len) st_sc1(outc + gp, acc[d].x);

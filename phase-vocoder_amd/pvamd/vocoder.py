@@ -200,19 +200,23 @@ class PhaseVocoder:
         return out
 
     def process(self, x, frames: int | None = None, n_samples: int | None = None, spec=None,
-                out=None, stream=None):
-        """analysis -> processing -> resynthesis; returns (out, spec)."""
+                out=None, stream=None, spectrum: bool = True):
+        """analysis -> processing -> resynthesis; returns (out, spec).  spectrum=False (single
+        launch only, pv_info.single_launch): no spectrum is written, spec is None."""
         x = self._as2d(x)
         C, n = x.shape
         n_samples = n if n_samples is None else n_samples
         frames = self.num_frames(n_samples) if frames is None else frames
-        if spec is None:
+        if not spectrum and spec is not None:
+            raise ValueError("spectrum=False with a spec buffer")
+        if spectrum and spec is None:
             spec = self.alloc_spec(C, frames)
         if out is None:
             out = self.alloc_out(C, frames)
         self._call(self._L.pv_process(self._h, _ptr(x), x.stride(0), n_samples, C, frames,
-                                      _ptr(spec), spec.stride(0) // 2, _ptr(out), out.stride(0),
-                                      self._stream(stream)), "pv_process")
+                                      _ptr(spec) if spec is not None else None,
+                                      spec.stride(0) // 2 if spec is not None else 0, _ptr(out),
+                                      out.stride(0), self._stream(stream)), "pv_process")
         return out, spec
 
     # -------------------------------------------------------------- reference per-frame API

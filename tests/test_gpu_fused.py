@@ -116,3 +116,25 @@ def test_fused_odd_output_stride_and_offset_input(cuda):
     dense, _ = pv.process(to_dev(xs))
     assert torch.equal(out, dense)
     assert torch.all(big[:, olen:] == 7.0)
+
+
+def test_fused_without_spectrum_output(cuda):
+    """pv_process with spec = NULL on the single launch (SURVEY §8(d) fused mode: the rows
+    are consumed on chip): the same output bits as with the spectrum written; the split path
+    refuses a missing spectrum buffer."""
+    import torch
+    from pvamd import _lib
+    x = synth(44100 * 3, 31)
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=600)
+    assert pv.single_launch
+    out1, spec = pv.process(to_dev(x))
+    out2, none = pv.process(to_dev(x), spectrum=False)
+    assert none is None and spec is not None
+    assert torch.equal(out1, out2)
+    ref = pvref.std_process(x, 1024, 4, ord("p"), 2.0)
+    assert rms(out2.cpu().numpy()[0], ref) <= RMS_TOL
+    split = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=600)
+    assert not split.single_launch
+    with pytest.raises(Exception):
+        split.process(to_dev(x), spectrum=False)
+    assert _lib.lib() is not None
