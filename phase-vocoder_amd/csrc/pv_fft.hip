@@ -4,9 +4,10 @@
 //
 // The reference runs log2(N) single-block launches per transform (GPU_FFT, one radix-2
 // stage each, ping-ponging through global memory).  Here:
-//   N in [128, 2048]: one transform per wavefront, the register-blocked Stockham engine of
+//   N in [128, 1024]: one transform per wavefront, the register-blocked Stockham engine of
 //     the phase-vocoder kernels (fft_run, pv_device.hpp): the same radix-2 butterflies
 //     with table twiddles, log2(N/64) stages per register pass, an LDS exchange per pass.
+//   N = 2048: the same passes over two waves per transform (k_fft2w).
 //   N in [2, 64]: one transform per LANE, every stage in registers (k_fft_reg); the
 //     per-stage LDS form (the reference's FftIteration in LDS, one transform per wave)
 //     remains for buffers that are not 16-byte aligned.
@@ -140,6 +141,146 @@ __global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, 
     }
 }
 
+
+// N = 2048: two waves per transform (128 "lanes" x E = 16 points: the register budget of the
+// N = 1024 kernel, which one wave holding 32 points per lane does not have — that form ran
+// at 1 wave/SIMD, 3.5 TB/s).  Radix-16, 16, 8 Stockham passes, each pass's radix-2 stages in
+// registers exactly as fft_pass (stage-major table twiddles W(m, Ns) = tw[Ns - 1 + m], W = 1 /
+// -i in the first two stages), exchanges through one padded LDS tile per transform with a
+// workgroup barrier (the two waves of a transform), the last pass's outputs stored straight
+// from registers (for a fixed register they are 128 consecutive points: coalesced).
+// A workgroup = 2 transforms x 2 waves.
+constexpr int kF2L = 2048, kF2NL = 128, kF2E = kF2L / kF2NL;
+__host__ __device__ constexpr int f2w_slot(int p) { return p + (p >> 4); }  // 1 pad per 16 points
+constexpr int kF2Tile = f2w_slot(kF2L - 1) + 1;
+
+template <int P, bool INV>
+__device__ __forceinline__ void fft2w_pass(f2v (&a)[kF2E], const float2* tw, const float2 (&tw0)[16], int vl) {
+    constexpr int L = kF2L, NL = kF2NL, E = kF2E;
+    constexpr int S = 1 << (4 * P);
+    constexpr int r = cmin(4, ilog2c(L) - 4 * P);
+    constexpr int R = 1 << r;
+    constexpr int NG = E / R;
+#pragma unroll
+    for (int st = 0; st < r; ++st) {
+        const int Ns = S << st;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int jm = (vl + NL * g) & (S - 1);
+            f2v b[R];
+#pragma unroll
+            for (int sb = 0; sb < R / 2; ++sb) {
+                const int br = bitrevc(sb & ((1 << st) - 1), st);
+                const f2v top = a[g * R + sb];
+                const f2v bot = a[g * R + sb + R / 2];
+                if (P == 0 && Ns == 2 && br != 0) {  // W = exactly -i (+i when INV)
+                    b[2 * sb] = pk_add_swp<INV>(top, bot);
+                    b[2 * sb + 1] = pk_add_swp<!INV>(top, bot);
+                    continue;
+                }
+                f2v t;
+                if (Ns == 1 || (P == 0 && Ns == 2)) {
+                    t = bot;
+                } else if constexpr (P == 0) {
+                    const float2 w = tw0[(Ns - 1) + br];
+                    t = cmul_v<INV, true>(bot, f2v{w.x, w.y});
+                } else if constexpr (P == 1) {
+                    const float2 w = lds_ld(&tw[(Ns - 1) + jm + S * br]);
+                    t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
+                } else {  // pass 2: from the global table (L2), see k_fft2w
+                    const float2 w = tw[(Ns - 1) + jm + S * br];
+                    t = cmul_v<INV, false>(bot, f2v{w.x, w.y});
+                }
+                b[2 * sb] = top + t;
+                b[2 * sb + 1] = top - t;
+            }
+#pragma unroll
+            for (int q = 0; q < R; ++q) a[g * R + q] = b[q];
+        }
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void fft2w_store(const f2v (&a)[kF2E], float2* tile, int vl) {
+    constexpr int L = kF2L, NL = kF2NL, E = kF2E;
+    constexpr int S = 1 << (4 * P);
+    constexpr int r = cmin(4, ilog2c(L) - 4 * P);
+    constexpr int R = 1 << r;
+#pragma unroll
+    for (int g = 0; g < E / R; ++g) {
+        const int j = vl + NL * g;
+        const int J = (j / S) * R * S + (j & (S - 1));
+#pragma unroll
+        for (int f = 0; f < R; ++f) tile[f2w_slot(J + S * bitrevc(f, r))] = make_float2(a[g * R + f].x, a[g * R + f].y);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void fft2w_load(f2v (&a)[kF2E], const float2* tile, int vl) {
+    constexpr int L = kF2L, NL = kF2NL, E = kF2E;
+    constexpr int r = cmin(4, ilog2c(L) - 4 * P);
+    constexpr int R = 1 << r;
+#pragma unroll
+    for (int g = 0; g < E / R; ++g)
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float2 v = lds_ld(&tile[f2w_slot(vl + NL * g + q * (L / R))]);
+            a[g * R + q] = f2v{v.x, v.y};
+        }
+}
+
+template <bool INV>
+__global__ __launch_bounds__(256) void k_fft2w(const float2* __restrict__ in, float2* out,
+                                                const float2* __restrict__ tw, int batch) {
+    constexpr int L = kF2L, NL = kF2NL, E = kF2E;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // LDS: the stage-major entries of pass 1 (stages Ns = 16 .. 128: entries < 256) and one
+    // tile per transform; pass 2's twiddles (Ns = 256 .. 1024) come from the global table
+    // (L2-resident) so that 4 workgroups fit a CU (with the whole table in LDS: 3)
+    float2* twl = reinterpret_cast<float2*>(smem);  // 256 stage-major twiddles
+    float2* tiles = twl + 256;                      // 2 x kF2Tile
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tloc = w >> 1;                  // transform of the workgroup
+    const int vl = ((w & 1) << 6) | (tid & 63);  // lane of the transform, 0..127
+    const long long b = (long long)blockIdx.x * 2 + tloc;
+    const bool live = b < batch;             // (no early return: the waves meet at barriers)
+    f2v a[E];
+    if (live) {
+        const float2* src = in + b * L + vl;
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const float2 v = src[NL * q];
+            a[q] = f2v{v.x, v.y};
+        }
+    }
+    float2 tw0[16];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) tw0[i] = tw[i];
+    tw0[15] = make_float2(1.0f, 0.0f);
+    twl[tid] = tw[tid];  // entries 0 .. 255: pass 0 (tw0) and pass 1
+    float2* tile = tiles + tloc * kF2Tile;
+    __syncthreads();
+    fft2w_pass<0, INV>(a, twl, tw0, vl);
+    fft2w_store<0>(a, tile, vl);
+    __syncthreads();
+    fft2w_load<1>(a, tile, vl);
+    fft2w_pass<1, INV>(a, twl, tw0, vl);
+    __syncthreads();  // every pass-1 read of the tile before it is overwritten
+    fft2w_store<1>(a, tile, vl);
+    __syncthreads();
+    fft2w_load<2>(a, tile, vl);
+    fft2w_pass<2, INV>(a, tw, tw0, vl);
+    // last pass (S = 256, R = 8): register g R + f holds point vl + 128 g + 256 bitrev3(f)
+    if (live) {
+        float2* dst = out + b * L + vl;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int f = 0; f < 8; ++f) dst[NL * g + 256 * bitrevc(f, 3)] = make_float2(a[g * 8 + f].x, a[g * 8 + f].y);
+    }
+}
+
 hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const float2* tw, int batch,
                       hipStream_t s) {
     const dim3 grid((unsigned)((batch + 3) / 4)), block(256);
@@ -154,7 +295,13 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
         case 256: PV_FFT_L(256); break;
         case 512: PV_FFT_L(512); break;
         case 1024: PV_FFT_L(1024); break;
-        case 2048: PV_FFT_L(2048); break;
+        case 2048: {
+            const dim3 g2((unsigned)((batch + 1) / 2));
+            const size_t lds = sizeof(float2) * (256 + 2 * kF2Tile);
+            if (inverse) hipLaunchKernelGGL((k_fft2w<true>), g2, block, lds, s, in, out, tw, batch);
+            else hipLaunchKernelGGL((k_fft2w<false>), g2, block, lds, s, in, out, tw, batch);
+            break;
+        }
         default: {
             if (n < 2 || n > 64 || (n & (n - 1))) return hipErrorInvalidValue;
             // in-place use reads each lane's transform completely before writing it: safe;
