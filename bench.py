@@ -266,14 +266,24 @@ def main():
     if compat:
         args.layout = "natural"  # REF_COMPAT rows: the 2N bins of kernel.cu:337
     layout = PV_SPEC_PACKED if args.layout == "packed" else PV_SPEC_NATURAL
-    pv = PhaseVocoder(N, effect, scale, hop_div, mode=REF_COMPAT if compat else STANDARD, max_channels=C,
-                      max_frames=pv_frames(n, N // hop_div), device=local, spec_layout=layout)
+    # under a process group only rank 0 builds the constant tables; the other ranks' handles
+    # start without any (tables_external) and compute with what the broadcast delivers
+    mk = dict(mode=REF_COMPAT if compat else STANDARD, device=local, spec_layout=layout)
+    pv = PhaseVocoder(N, effect, scale, hop_div, max_channels=C, max_frames=pv_frames(n, N // hop_div),
+                      tables_external=distributed and rank != 0, **mk)
     frames = pv.num_frames(n)
     tables = None
     if distributed:  # init-time RCCL broadcast of rank 0's tables (north_star); not timed
         from pvamd.dist import broadcast_tables
-        same = broadcast_tables(pv, src=0)
-        tables = {"bytes": int(pv.export_tables().numel()), "bit_identical_to_local": same}
+        # the check only: a one-frame handle built locally, compared with what arrived
+        ref = PhaseVocoder(N, effect, scale, hop_div, max_channels=1, max_frames=1, **mk) if rank != 0 else None
+        same = broadcast_tables(pv, src=0, local=ref)
+        t_same = torch.tensor([0.0 if same else 1.0], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t_same, op=dist.ReduceOp.MAX)
+        tables = {"bytes": pv.tables_bytes(), "built_on": "rank 0 only (the other ranks' handles: tables_external)",
+                  "received_by_ranks": world - 1, "bit_identical_to_local": bool(t_same.item() == 0.0)}
+        if ref is not None:
+            ref.close()
     threads, _ = cpu_share()
     t_gen = time.perf_counter()
     x_host = synth_channels_np(C, n, 20240 + rank * C, threads)

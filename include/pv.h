@@ -50,12 +50,14 @@
 extern "C" {
 #endif
 
-#define PV_ABI_VERSION 4  /* 2: pv_config.window / nan_faithful, pv_set_window;
+#define PV_ABI_VERSION 5  /* 2: pv_config.window / nan_faithful, pv_set_window;
                              3: pv_info.single_launch / single_launch_frames / lane_constants;
                              4: leading abi_version in pv_config / pv_info (checked: a caller
                                 built against another header gets PV_ERR_ARG, not a
                                 misread struct), pv_config.spec_layout, the chained path
-                                and pv_check_device removed */
+                                and pv_check_device removed;
+                             5: pv_config.tables_external, pv_process(spec = NULL) on the
+                                single launch */
 
 typedef struct pv_handle pv_handle;
 
@@ -118,6 +120,13 @@ typedef struct pv_config {
                          in the reference (kernel.cu:101-109), which poisons that frame's
                          resynthesis; 0 (default) gives phase 0 (SURVEY.md §8c deviation 4) */
     int spec_layout;  /* pv_spec_layout (STANDARD only; REF_COMPAT accepts 0)              */
+    int tables_external; /* 1: the handle's constant tables (windows, gains, twiddles, unwrap
+                            and pitch maps) are not built here — the device tables start
+                            zeroed and every compute call returns PV_ERR_ARG until
+                            pv_import_tables loads a blob (a non-root rank of a multi-GPU
+                            job receives rank 0's over RCCL, pvamd.dist.broadcast_tables);
+                            0 (default): built by pv_create.  Batch handles only (pv_rt /
+                            harmoniser reject it) */
 } pv_config;
 
 typedef struct pv_info {

@@ -138,6 +138,7 @@ struct pv_handle {
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
+    int tables_ready = 1;  // 0: pv_config.tables_external until pv_import_tables
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
     int packed = 0;  // PV_SPEC_PACKED rows (STANDARD)
     float scale = 1.0f, rho = 1.0f, inv_q = 1.0f;
@@ -162,6 +163,18 @@ struct pv_handle {
 
 namespace {
 
+template <typename T>
+pv_status upload(T** dst, const std::vector<T>& src);
+// a constant table of the handle: uploaded, or (pv_config.tables_external) allocated zeroed
+// for pv_import_tables to fill — the host copy never reaches the device
+template <typename T>
+pv_status upload_table(T** dst, const std::vector<T>& src, bool external) {
+    if (!external) return upload(dst, src);
+    const size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
+    PV_HIP(hipMalloc((void**)dst, bytes));
+    PV_HIP(hipMemset(*dst, 0, bytes));
+    return PV_OK;
+}
 template <typename T>
 pv_status upload(T** dst, const std::vector<T>& src) {
     PV_HIP(hipMalloc((void**)dst, sizeof(T) * (src.empty() ? 1 : src.size())));
@@ -251,6 +264,8 @@ int nruns_of(const pv_handle* h, int frames) { return (frames + h->F - 1) / h->F
 
 pv_status check_common(const pv_handle* h, int channels, int frames) {
     if (!h) return fail(PV_ERR_ARG, "null handle");
+    if (!h->tables_ready)
+        return fail(PV_ERR_ARG, "tables_external handle: no tables yet (pv_import_tables first)");
     if (channels < 0 || frames < 0) return fail(PV_ERR_ARG, "negative channels/frames");
     if (channels > h->cfg.max_channels || frames > h->cfg.max_frames)
         return fail(PV_ERR_ARG, "channels/frames exceed the handle's capacity (max_channels, max_frames)");
@@ -646,6 +661,12 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         return s;
     };
 
+    // ---- constant tables (pv_config.tables_external: allocated zeroed, filled only by
+    // pv_import_tables — a non-root rank of a multi-GPU job receives rank 0's)
+    const bool ext_tables = cfg->tables_external != 0;
+    h->tables_ready = ext_tables ? 0 : 1;
+    auto upload_tab = [&](auto** dst, const auto& v) { return upload_table(dst, v, ext_tables); };
+
     // ---- windows and gains
     std::vector<float> win, gain(N);
     if (h->mode == PV_MODE_STANDARD) {
@@ -662,24 +683,24 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         else hamming_ref(N, win);
         for (int i = 0; i < N; ++i) gain[i] = win[i] / (float)N;  // kernel.cu:380 /N, :406 window
     }
-    if ((st = upload(&h->d_win, win)) != PV_OK) return bail(st);
-    if ((st = upload(&h->d_gain, gain)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_win, win)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_gain, gain)) != PV_OK) return bail(st);
 
     // ---- twiddles
     std::vector<float2> t;
     fft_table(h->L_ana, t);
-    if ((st = upload(&h->d_tw_ana, t)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_tw_ana, t)) != PV_OK) return bail(st);
     split_twiddles(2 * h->L_ana, t);
-    if ((st = upload(&h->d_tws_ana, t)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_tws_ana, t)) != PV_OK) return bail(st);
     fft_table(h->L_syn, t);
     if (tw_syn_len(h->L_syn) > h->L_syn) {
         std::vector<float2> t3;
         fft_table(h->L_syn, t3, true);
         t.insert(t.end(), t3.begin(), t3.end());
     }
-    if ((st = upload(&h->d_tw_syn, t)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_tw_syn, t)) != PV_OK) return bail(st);
     split_twiddles(N, t);
-    if ((st = upload(&h->d_tws_syn, t)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_tws_syn, t)) != PV_OK) return bail(st);
 
     // ---- unwrap tables and the rational output-phase factor rho = p/q
     const int B = h->bins;
@@ -720,8 +741,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         unsigned long long v = ((pn % qd) * ((unsigned long long)jk[k] % qd)) % qd;
         jkm[k] = (unsigned)v;
     }
-    if ((st = upload(&h->d_ek, ek)) != PV_OK) return bail(st);
-    if ((st = upload(&h->d_jk_mod, jkm)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_ek, ek)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_jk_mod, jkm)) != PV_OK) return bail(st);
     {
         // per-lane unwrap constants (the synthesis keeps them in two registers): every bin
         // k < L repeats bin k mod 64, and bin L's e equals bin 0's
@@ -745,8 +766,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
             cnt[kp]++;
         }
     }
-    if ((st = upload(&h->d_src_first, first)) != PV_OK) return bail(st);
-    if ((st = upload(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_src_first, first)) != PV_OK) return bail(st);
+    if ((st = upload_tab(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
 
     // ---- single-launch path (q = 1): no halo frame, so runs can be as short as the overlap
     // tail allows (F hs >= N - hs) to give a single stream enough waves; PV_FUSED=0 disables
@@ -880,6 +901,7 @@ extern "C" {
 
 pv_status pv_export_tables(const pv_handle* h, void* dst, size_t cap, size_t* bytes, void* stream) {
     if (!h || !bytes) return fail(PV_ERR_ARG, "null argument");
+    if (dst && !h->tables_ready) return fail(PV_ERR_ARG, "tables_external handle: no tables to export yet");
     size_t total = sizeof(TableBlobHeader);
     for (const auto& sg : table_segments(h)) total += align16(sg.bytes);
     *bytes = total;
@@ -918,6 +940,7 @@ pv_status pv_import_tables(pv_handle* h, const void* src, size_t bytes, void* st
         off += align16(sg.bytes);
     }
     PV_HIP(hipStreamSynchronize(s));
+    h->tables_ready = 1;
     return PV_OK;
 }
 
@@ -1064,6 +1087,7 @@ pv_status pv_rt_reset(pv_rt* rt, void* stream) {
 
 pv_status pv_rt_create(const pv_config* cfg, int channels, pv_rt** out) {
     if (!cfg || !out) return fail(PV_ERR_ARG, "null argument");
+    if (cfg->tables_external) return fail(PV_ERR_UNSUPPORTED, "tables_external: batch handles only");
     *out = nullptr;
     if (cfg->mode != PV_MODE_STANDARD)
         return fail(PV_ERR_UNSUPPORTED, "real-time mode runs the STANDARD pipeline only");
@@ -1295,6 +1319,7 @@ void pv_harmonizer_destroy(pv_harmonizer* hz) {
 
 pv_status pv_harmonizer_create(const pv_config* cfg, const float* ratios, int voices, pv_harmonizer** out) {
     if (!cfg || !ratios || !out) return fail(PV_ERR_ARG, "null argument");
+    if (cfg->tables_external) return fail(PV_ERR_UNSUPPORTED, "tables_external: batch handles only");
     *out = nullptr;
     if (voices <= 0 || voices > 64) return fail(PV_ERR_ARG, "voices must be in [1, 64]");
     if (cfg->mode != PV_MODE_STANDARD) return fail(PV_ERR_UNSUPPORTED, "the harmoniser runs the STANDARD pipeline");

@@ -16,7 +16,7 @@ PV_TIME_SHIFT, PV_PITCH_SHIFT = ord("t"), ord("p")
 PV_MODE_REF_COMPAT, PV_MODE_STANDARD = 0, 1
 PV_WINDOW_DEFAULT, PV_WINDOW_HAMMING_REF, PV_WINDOW_HANN_REF = 0, 1, 2
 PV_SPEC_NATURAL, PV_SPEC_PACKED = 0, 1
-ABI_VERSION = 4  # PV_ABI_VERSION of include/pv.h (pv_config / pv_info lead with it)
+ABI_VERSION = 5  # PV_ABI_VERSION of include/pv.h (pv_config / pv_info lead with it)
 
 
 class PVError(RuntimeError):
@@ -29,7 +29,8 @@ class pv_config(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_int), ("n_samps", ctypes.c_int), ("hop_div", ctypes.c_int), ("effect", ctypes.c_int),
                 ("scale", ctypes.c_float), ("mode", ctypes.c_int), ("max_channels", ctypes.c_int),
                 ("max_frames", ctypes.c_int), ("device", ctypes.c_int), ("window", ctypes.c_int),
-                ("nan_faithful", ctypes.c_int), ("spec_layout", ctypes.c_int)]
+                ("nan_faithful", ctypes.c_int), ("spec_layout", ctypes.c_int),
+                ("tables_external", ctypes.c_int)]
 
 
 class pv_info(ctypes.Structure):
@@ -42,11 +43,11 @@ class pv_info(ctypes.Structure):
 
 
 def config(n_samps, hop_div, effect, scale, mode, max_channels, max_frames, device=0, window=PV_WINDOW_DEFAULT,
-           nan_faithful=0, spec_layout=PV_SPEC_NATURAL) -> pv_config:
+           nan_faithful=0, spec_layout=PV_SPEC_NATURAL, tables_external=0) -> pv_config:
     """A pv_config for this ABI (abi_version filled in)."""
     return pv_config(ABI_VERSION, int(n_samps), int(hop_div), int(effect), float(scale), int(mode),
                      int(max_channels), int(max_frames), int(device), int(window), int(nan_faithful),
-                     int(spec_layout))
+                     int(spec_layout), int(tables_external))
 
 
 def new_info() -> pv_info:

@@ -24,20 +24,31 @@ def broadcast_blob(blob, src: int = 0, group=None):
     return blob
 
 
-def broadcast_tables(pv, src: int = 0, group=None) -> bool:
+def broadcast_tables(pv, src: int = 0, group=None, local=None):
     """Rank `src` exports its handle's tables (pv_export_tables: one device blob); every
-    other rank imports them (pv_import_tables).  With the nccl backend (RCCL over xGMI) the
-    device blob is broadcast as is; a CPU backend (gloo: the CPU multi-process tests, a
-    rehearsal on one GPU) stages it through host memory.  Returns True when this rank's own
-    tables were already bit-identical to the received ones."""
+    other rank imports them (pv_import_tables).  The receiving ranks' handles are normally
+    created with `tables_external=True`: they build no tables, so what they compute with is
+    exactly what arrived over the wire.  With the nccl backend (RCCL over xGMI) the device
+    blob is broadcast as is; a CPU backend (gloo: the CPU multi-process tests, a rehearsal on
+    one GPU) stages it through host memory.  Returns whether the received blob is
+    bit-identical to this rank's own tables — `local` (a handle of the same configuration
+    that built them) or, on `src`, the sent blob itself — or None when there is nothing
+    local to compare with."""
     import torch
     import torch.distributed as dist
-    mine = pv.export_tables()
-    wire = mine if dist.get_backend(group) == "nccl" else mine.cpu()
-    blob = wire.clone() if dist.get_rank(group) == src else torch.empty_like(wire)
+    is_src = dist.get_rank(group) == src
+    nccl = dist.get_backend(group) == "nccl"
+    dev = getattr(pv, "blob_device", None) or f"cuda:{pv.device}"
+    if is_src:
+        mine = pv.export_tables()
+        blob = mine if nccl else mine.cpu()
+    else:
+        blob = torch.empty(pv.tables_bytes(), dtype=torch.uint8, device=dev if nccl else "cpu")
     broadcast_blob(blob, src=src, group=group)
-    blob = blob.to(mine.device)
-    same = bool(torch.equal(blob, mine))
-    if dist.get_rank(group) != src:
+    blob = blob.to(dev)
+    if not is_src:
         pv.import_tables(blob)
-    return same
+    ref = pv if is_src else local
+    if ref is None:
+        return None
+    return bool(torch.equal(blob, ref.export_tables()))

@@ -43,17 +43,18 @@ class PhaseVocoder:
                  hop: int = 2, *, mode: str = REF_COMPAT, max_channels: int = 1,
                  max_frames: int = 4096, device: int = 0, exit_on_error: bool = False,
                  window: int = _lib.PV_WINDOW_DEFAULT, nan_faithful: bool = False,
-                 spec_layout: int = _lib.PV_SPEC_NATURAL):
+                 spec_layout: int = _lib.PV_SPEC_NATURAL, tables_external: bool = False):
         """window: PV_WINDOW_DEFAULT (the mode's), PV_WINDOW_HAMMING_REF or
         PV_WINDOW_HANN_REF (the 1-argument constructor's, phaseVocoder.h:64-66; see
         `single_arg`); nan_faithful: REF_COMPAT atanf(0/0) = NaN (kernel.cu:101-109);
         spec_layout: PV_SPEC_NATURAL or PV_SPEC_PACKED (STANDARD: bin N/2 folded into slot 0,
-        see `unpack_spec`)."""
+        see `unpack_spec`); tables_external: build no tables — `import_tables` (or
+        pvamd.dist.broadcast_tables) must load them before any compute call."""
         self.exit_on_error = exit_on_error
         eff = effect if isinstance(effect, int) else ord(effect)
         m = PV_MODE_REF_COMPAT if mode == REF_COMPAT else PV_MODE_STANDARD
         cfg = _lib.config(samples, hop, eff, scaleFactor, m, max_channels, max_frames, device, window,
-                          1 if nan_faithful else 0, spec_layout)
+                          1 if nan_faithful else 0, spec_layout, 1 if tables_external else 0)
         self.window = int(window)
         h = ctypes.c_void_p()
         self._L = _lib.lib()
@@ -239,6 +240,12 @@ class PhaseVocoder:
                                           self._stream()), "resynthesis_CUFFT")
 
     # -------------------------------------------------------------- shared tables
+    def tables_bytes(self) -> int:
+        """Size of this handle's table blob (pv_export_tables with no destination)."""
+        n = ctypes.c_size_t()
+        self._call(self._L.pv_export_tables(self._h, None, 0, ctypes.byref(n), None), "pv_export_tables")
+        return int(n.value)
+
     def export_tables(self):
         """Constant tables as one uint8 CUDA tensor (header + windows + twiddles + ...)."""
         torch = _torch()

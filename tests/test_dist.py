@@ -64,14 +64,20 @@ def test_channel_shard_uneven():
 
 
 class _FakeHandle:
-    """Stands in for PhaseVocoder's export_tables / import_tables on CPU."""
+    """Stands in for PhaseVocoder's export_tables / import_tables on CPU; external=True is a
+    handle created with tables_external (no tables until an import)."""
+    blob_device = "cpu"
 
-    def __init__(self, rank):
+    def __init__(self, rank, external=False):
         g = torch.Generator().manual_seed(99 if rank == 0 else 100 + rank)
-        self.tables = torch.randint(0, 256, (4096,), dtype=torch.uint8, generator=g)
+        self.tables = None if external else torch.randint(0, 256, (4096,), dtype=torch.uint8, generator=g)
         self.imported = 0
 
+    def tables_bytes(self):
+        return 4096
+
     def export_tables(self):
+        assert self.tables is not None, "tables_external handle: nothing to export"
         return self.tables.clone()
 
     def import_tables(self, blob):
@@ -83,20 +89,25 @@ def _tables_worker(rank, world, port, results):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        h = _FakeHandle(rank)
-        same = broadcast_tables(h, src=0)
+        h = _FakeHandle(rank, external=rank != 0)
+        local = _FakeHandle(0) if rank == 2 else None  # rank 2 compares with a local build
+        same = broadcast_tables(h, src=0, local=local)
         results[rank] = (same, h.imported, h.tables.sum().item(), int(h.tables[:8].sum()))
     finally:
         dist.destroy_process_group()
 
 
 def test_broadcast_tables_gloo():
-    """broadcast_tables over gloo: rank 0 keeps its tables, the others import rank 0's."""
+    """broadcast_tables over gloo: rank 0 keeps its tables; the others start with none
+    (tables_external) and hold exactly rank 0's after the import; a rank given a locally
+    built handle reports whether the received blob equals it."""
     world, port = 3, _free_port()
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_tables_worker, args=(world, port, results), nprocs=world, join=True)
     assert results[0][0] is True and results[0][1] == 0
     for r in range(1, world):
-        assert results[r][0] is False and results[r][1] == 1
+        assert results[r][1] == 1
         assert results[r][2:] == results[0][2:]
+    assert results[1][0] is None       # nothing local to compare with
+    assert results[2][0] is True       # its local build (seed 99) equals rank 0's

@@ -1,7 +1,8 @@
 """Multi-GPU readiness on one GPU: two fresh child processes, one per rank,
 gloo process group (the 8-GPU node runs the same code over RCCL).  Each rank takes its
 contiguous channel shard, receives rank 0's real pv_export_tables blob through
-pvamd.dist.broadcast_tables (rank 1 starts from deliberately damaged tables, so the
+pvamd.dist.broadcast_tables (rank 1's handle is created with tables_external: it builds no
+tables and refuses to compute until the broadcast delivers rank 0's, so the
 import must take effect), runs pv_process on its shard and checks it against the oracle."""
 import json
 import os
@@ -51,4 +52,7 @@ def test_two_rank_shards_with_table_broadcast(cuda):
         assert max(d["rms"]) <= 1e-5, d
         assert d["rms_max_all_ranks"] <= 1e-5
     assert covered == list(range(total))
-    assert res[0]["same_before"] is True and res[1]["same_before"] is False
+    # rank 0 sent its own tables; rank 1 had none (tables_external: it refused to compute
+    # before the broadcast) and computed with exactly what arrived
+    assert res[0]["same_before"] is True and res[1]["same_before"] is None
+    assert res[1]["refused_without_tables"] is True
