@@ -309,6 +309,41 @@ __global__ __launch_bounds__(256) void k_prod_pol(const float* __restrict__ x, f
     if (acc.x == -1.0f) spec[0] = f2(pad[lane]);
 }
 
+// prod with synthetic VALU work per frame: K rounds of 16 independent v_fma_f32 chains
+// (16 K fmas, ~2.25 cycles each per wave at high occupancy): does the 8-frame-run map keep
+// its advantage when the frame also computes?
+template <int FF, int K>
+__global__ __launch_bounds__(256, 5) void k_prod_cmp(const float* __restrict__ x, f2* __restrict__ spec) {
+    __shared__ float pad[7500];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y, t0 = (blockIdx.x * 4 + w) * FF;
+    const float* xc = x + c * LDX;
+    f2 acc = f2((float)lane);
+    if (threadIdx.x == 0) pad[0] = acc.x;
+    auto src = [&](int u) { return xc + (long long)(t0 + u) * 256 + 768 + 2 * lane; };
+    f2 a = *reinterpret_cast<const f2*>(src(0)), b = *reinterpret_cast<const f2*>(src(0) + 128);
+    for (int u = 0; u < FF; ++u) {
+        const int un = u + 1 < FF ? u + 1 : u;
+        const f2 an = *reinterpret_cast<const f2*>(src(un)), bn = *reinterpret_cast<const f2*>(src(un) + 128);
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = a.x * (float)(i + 1) + b.y;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = __builtin_fmaf(v[i], 0.999f, b.x);
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sum += v[i];
+        acc += a * b + sum;
+        f2* row = spec + ((long long)c * FRAMES + t0 + u) * S;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) __builtin_nontemporal_store(acc + (float)i, &row[lane + 64 * i]);
+        a = an; b = bn;
+    }
+    if (acc.x == -1.0f) spec[0] = f2(pad[lane]);
+}
+
 template <typename Fn>
 static double timeit(Fn f, int reps) {
     hipEvent_t a, b;
@@ -341,6 +376,19 @@ int main() {
     const int R = 10;
     const dim3 gp(NRUNS / 4, C), gi(NRUNS / 4, C);
     const char* only = getenv("MIX_ONLY");
+    if (only && only[0] == '5') {
+        for (int r2 = 0; r2 < 2; ++r2) {
+            rep("cmp0_F88", timeit([&] { k_prod_cmp<88, 0><<<gp, 256>>>(x, spec); }, R));
+            rep("cmp0_F8", timeit([&] { k_prod_cmp<8, 0><<<dim3(FRAMES / 32, C), 256>>>(x, spec); }, R));
+            rep("cmp24_F88", timeit([&] { k_prod_cmp<88, 24><<<gp, 256>>>(x, spec); }, R));
+            rep("cmp24_F8", timeit([&] { k_prod_cmp<8, 24><<<dim3(FRAMES / 32, C), 256>>>(x, spec); }, R));
+            rep("cmp44_F88", timeit([&] { k_prod_cmp<88, 44><<<gp, 256>>>(x, spec); }, R));
+            rep("cmp44_F8", timeit([&] { k_prod_cmp<8, 44><<<dim3(FRAMES / 32, C), 256>>>(x, spec); }, R));
+            rep("cmp60_F88", timeit([&] { k_prod_cmp<88, 60><<<gp, 256>>>(x, spec); }, R));
+            rep("cmp60_F8", timeit([&] { k_prod_cmp<8, 60><<<dim3(FRAMES / 32, C), 256>>>(x, spec); }, R));
+        }
+        return 0;
+    }
     if (only && only[0] == '4') {
         for (int r2 = 0; r2 < 2; ++r2) {
             rep("pol_st_nt", timeit([&] { k_prod_pol<1, false><<<gp, 256>>>(x, spec); }, R));
