@@ -31,7 +31,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.pv_abi_version() == _lib.ABI_VERSION == 4
+    assert L.pv_abi_version() == _lib.ABI_VERSION == 5
     assert L.pv_status_string(0) == b"PV_OK"
     assert L.pv_status_string(2) == b"PV_ERR_UNSUPPORTED"
 
