@@ -138,6 +138,7 @@ struct pv_handle {
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
+    int src_hi = 0;   // highest analysis bin any output bin reads (pitch map; L otherwise)
     int tables_ready = 1;  // 0: pv_config.tables_external until pv_import_tables
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
     int packed = 0;  // PV_SPEC_PACKED rows (STANDARD)
@@ -438,6 +439,28 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     p.tail_len = h->tail_len;
     p.seam_flags = h->d_seam_flags;
     p.packed = h->packed;
+    p.src_hi = h->src_hi;
+    p.nwg = (nruns + 3) / 4;
+    p.n4 = 0;
+    // one channel whose workgroups do not fill whole rounds of the 256 CUs (config 2: 862 =
+    // 3 x 256 + 94, so 94 CUs ran a 4th workgroup, 12 frames on their SIMDs against 9):
+    // exactly `rounds` workgroups per CU, some runs one frame longer (k_fused "balanced";
+    // PV_FUSED_BALANCE=0 turns it off).  The run boundaries move, so the seams' rounding
+    // does (<= 1e-6); the output depends only on the configuration.
+    {
+        constexpr int kRoundCUs = 256;  // MI355X
+        const int rounds = p.nwg / kRoundCUs;
+        const char* eb = std::getenv("PV_FUSED_BALANCE");
+        const bool on = !(eb && eb[0] == '0');
+        if (on && C == 1 && rounds >= 1 && p.nwg % kRoundCUs != 0) {
+            const int G = rounds * kRoundCUs;
+            const long long n4 = (long long)frames - 4LL * F * G;
+            if (n4 > 0 && n4 <= 4LL * G) {
+                p.nwg = G;
+                p.n4 = (int)n4;
+            }
+        }
+    }
 #ifdef PV_FUSED_STAMPS
     p.stamps = h->d_stamps;
 #endif
@@ -768,6 +791,12 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     }
     if ((st = upload_tab(&h->d_src_first, first)) != PV_OK) return bail(st);
     if ((st = upload_tab(&h->d_src_cnt, cnt)) != PV_OK) return bail(st);
+    h->src_hi = B - 1;
+    if (h->pitch) {
+        h->src_hi = -1;
+        for (int k = 0; k < B; ++k)
+            if (cnt[k] > 0) h->src_hi = std::max(h->src_hi, first[k] + cnt[k] - 1);
+    }
 
     // ---- single-launch path (q = 1): no halo frame, so runs can be as short as the overlap
     // tail allows (F hs >= N - hs) to give a single stream enough waves; PV_FUSED=0 disables

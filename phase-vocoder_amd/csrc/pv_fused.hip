@@ -49,7 +49,22 @@ struct FuGeo {
 // chip in one round (at 131 VGPRs, 3 per SIMD, a tenth of them ran as a second round:
 // config 2 fused 53.5-55.2 -> 45.2-46.2 us)
 template <int L, int MODE, int DT>
-__global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
+// waves per SIMD k_fused is compiled for: 3 (<= 168 VGPRs; the balanced config-2 launch
+// holds exactly 3 workgroups per CU) — at 4 (<= 128) the L = 512 kernels spilled 6-12 VGPRs
+// to scratch; round 5 A/B: config 2 30.9 -> 30.1 us, and with the register split 29.6
+#ifndef PV_FUSED_WAVES
+#define PV_FUSED_WAVES 3
+#endif
+// 0: analyse every bin even without a spectrum output (A/B of the skip; same results)
+// 1: the real split straight from the FFT's last-pass registers (split_chunk_bp, as
+// k_std_analysis) instead of from a final image in LDS (0: the LDS-image split, A/B only)
+#ifndef PV_FUSED_BPSPLIT
+#define PV_FUSED_BPSPLIT 1
+#endif
+#ifndef PV_FUSED_SKIP_UNREAD
+#define PV_FUSED_SKIP_UNREAD 1
+#endif
+__global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
     using G_ = Geo<L>;
     using FG = FuGeo<L>;
     constexpr int E = G_::E;
@@ -82,9 +97,29 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
 #define PV_STAMP(slot_) ((void)0)
 #endif
     const int c = blockIdx.y;
-    const int run = blockIdx.x * 4 + w;
-    const int t0 = run * p.F;
-    const int nfr = max(0, min(p.F, p.frames - t0));  // real frames of this wave's run
+    // this wave's run: F frames, or (balanced, p.n4 > 0) F or F + 1.  Balanced: the launch is
+    // exactly `rounds` workgroups per CU (no CU holds one more than the others) and the n4
+    // long runs are spread over the workgroups (floor((k+1) n4 / nwg) - floor(k n4 / nwg) =
+    // 1 or 2 per workgroup) at wave positions rotated by the workgroup's dispatch round
+    // (linear id / 256): the workgroups a CU holds — k, k + 256, k + 512 with the
+    // dispatcher's round-robin over XCDs and CUs — put theirs on different SIMDs, so a SIMD
+    // runs at most 2 long runs (3 waves: 11 frames instead of 4 waves: 12).  Any other
+    // placement is still correct, only less balanced.
+    int t0, fw;
+    if (p.n4 > 0) {
+        const int k = blockIdx.x;
+        const long long a = (long long)k * p.n4 / p.nwg, b = (long long)(k + 1) * p.n4 / p.nwg;
+        const int m = (int)(b - a);
+        const int r = (int)((blockIdx.y * gridDim.x + blockIdx.x) >> 8) & 3;
+        int pre = 0;
+        for (int v = 0; v < w; ++v) pre += p.F + ((((v - r) & 3) < m) ? 1 : 0);
+        t0 = 4 * p.F * k + (int)a + pre;
+        fw = p.F + ((((w - r) & 3) < m) ? 1 : 0);
+    } else {
+        t0 = (blockIdx.x * 4 + w) * p.F;
+        fw = p.F;
+    }
+    const int nfr = max(0, min(fw, p.frames - t0));  // real frames of this wave's run
     const int hs = p.hs;
     const int TL = N - hs;
     float2* tile = tiles + w * G_::TILE;
@@ -177,7 +212,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
     __syncthreads();
     PV_STAMP(2);
 
-    for (int u = 0; u < p.F; ++u) {
+    for (int u = 0; u < fw; ++u) {
         const int t = t0 + u;
         if (u < nfr) {
             float2 z[E];
@@ -193,27 +228,48 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
             if (u == 0) PV_STAMP(10);  // frame 0's samples have landed (F <= 7)
             if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
             // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv.  The
-            // split reads the final image in LDS (the register split, split_chunk_bp, costs
-            // this kernel 2 VGPRs over 128 at L = 512: 3 waves/SIMD, or spills at 4; config 2
-            // +2-3 %)
+            // split takes the partner bins from the last pass's registers by a lane reversal
+            // (split_chunk_bp; bit-identical to the LDS-image split)
+#if PV_FUSED_BPSPLIT
+            fft_run<L, false, false>(z, tile, twl, tw0, lane);
+#else
             fft_run<L, false, true>(z, tile, twl, tw0, lane);
+#endif
             float2 sv[E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
+            // without a spectrum output only the bin pairs holding a bin some output bin reads
+            // are analysed (pitch 2.0: bins 0 .. 256 of 512, so 3 of 4 pairs and no bin L): a
+            // wave-uniform bound, the skipped bins' slots hold zeros that no gather reads
+            const int shi = (wspec || !PV_FUSED_SKIP_UNREAD) ? L : p.src_hi;
             // bin L (real: A = B = Z[0]) once, wave-uniformly, as k_std_analysis's bin_l_real:
             // its contract phase is +0 or pi, no atan2 (bit-identical to the generic bin)
-            {
+            if (shi >= L) {
                 float magL, phL;
+#if PV_FUSED_BPSPLIT
+                bin_l_real<L, true>(z, twsl, magL, phL);
+#else
                 bin_l_real_tile<L, true>(tile, twsl, magL, phL);
+#endif
                 sv[E] = make_float2(magL, phL);
                 if (wspec && !p.packed) __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
+            } else {
+                sv[E] = make_float2(0.0f, 0.0f);
             }
             // bins 0 .. E-1 in pairs: the phases of a pair through the packed-fp32 atan2
             // (atan2_pv2, bit-identical to atan2_pv per half)
             constexpr int CH = 2;
             static_for<0, E / CH>([&](auto ic) {
                 constexpr int i0 = decltype(ic)::value * CH;
+                if (64 * i0 > shi) {
+                    sv[i0] = sv[i0 + 1] = make_float2(0.0f, 0.0f);
+                    return;
+                }
                 float2 X[CH];
+#if PV_FUSED_BPSPLIT
+                split_chunk_bp<L, CH, true, i0, false>(z, twsl, lane, X);
+#else
                 split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
+#endif
                 float phs[CH];
                 {
                     const f2v ph2 = atan2_pv2(X[0].y, X[0].x, X[1].y, X[1].x);
@@ -289,7 +345,7 @@ __global__ __launch_bounds__(256, 4) void k_fused(FusedParams p) {
     __syncthreads();
     PV_STAMP(9);  // the workgroup's slowest wave has finished its frames (F <= 6)
 #endif
-    close_seams_inline<L, NS, D>(acc, tiles, w, lane, c, blockIdx.x, (p.nruns + 3) / 4, obase, p.F, hs, outc,
+    close_seams_inline<L, NS, D>(acc, tiles, w, lane, c, blockIdx.x, p.nwg, obase, fw, hs, outc,
                                  p.out_len, p.out_aligned != 0, p.tails, p.tail_len, p.seam_flags);
 #ifdef PV_FUSED_STAMPS
     {
@@ -343,7 +399,7 @@ static hipError_t launch_fused_m(int L, int dt, dim3 grid, const FusedParams& p,
 // mode: 0 STANDARD stretch, 2 STANDARD pitch (q = 1 only; the caller checks); pitch >= 1
 // takes the MODE 3 kernels (one source per bin: the select-free gather, as k_synthesis)
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s) {
-    const dim3 grid((p.nruns + 3) / 4, channels);
+    const dim3 grid(p.nwg, channels);
     const int dt = p.hs / 128;
     if (mode == 2 && p.rho >= 1.0f) return launch_fused_m<3>(L, dt, grid, p, s);
     return mode == 2 ? launch_fused_m<2>(L, dt, grid, p, s) : launch_fused_m<0>(L, dt, grid, p, s);

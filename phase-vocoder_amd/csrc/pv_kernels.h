@@ -103,6 +103,13 @@ struct FusedParams {
     int tail_len;
     int* seam_flags;                   // [C][nwg] arrival counters, 0 between launches
     int packed;                        // PV_SPEC_PACKED rows
+    int src_hi;                        // highest analysis bin an output bin reads (pitch > 1:
+                                       // about L / pitch): with spec == nullptr the bins above
+                                       // it are not analysed (nothing reads their phase)
+    int nwg;                           // workgroups per channel (grid.x)
+    int n4;                            // > 0: balanced runs — n4 of them have F + 1 frames
+                                       // (k_fused: which ones, so that no SIMD holds more than
+                                       // two of them); 0: every run F frames
 #ifdef PV_FUSED_STAMPS
     unsigned long long* stamps;        // diagnostic build only: kFusedStampSlots per wave
 #endif

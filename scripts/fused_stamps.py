@@ -58,7 +58,8 @@ def main():
     nw = 4 * (-(-nruns // 4))
     buf = np.zeros(nw * SLOTS, np.uint64)
     _lib.check(L.pv_debug_stamps(pv._h, buf.ctypes.data, buf.size), "pv_debug_stamps")
-    st = buf.reshape(nw, SLOTS)[:nruns].astype(np.int64)
+    st = buf.reshape(nw, SLOTS).astype(np.int64)
+    st = st[st[:, 0] != 0]  # the waves the launch had (a balanced launch has fewer than nruns)
     if len(sys.argv) > 2:
         np.save(sys.argv[2], st)  # raw stamps for offline analysis
     rt0, mt0, setup = st[:, 0], st[:, 1], st[:, 2]
@@ -74,7 +75,7 @@ def main():
     frame_d = np.diff(np.concatenate([setup[:, None], frames], axis=1), axis=1)
     res = {
         "launch_span_us": float((rt1.max() - t_min) * us),
-        "waves": int(nruns), "F": F, "steps": steps, "host_ms_per_step": dt * 1e3,
+        "waves": int(len(st)), "runs_uniform_F": int(nruns), "F": F, "steps": steps, "host_ms_per_step": dt * 1e3,
         "start_offset_us": {q: pct((rt0 - t_min) * us, q) for q in (0, 10, 50, 90, 100)},
         "setup_us": {q: pct((setup - rt0) * us, q) for q in (10, 50, 90, 100)},
         "frame_us": {f"frame{j}": {q: pct(frame_d[:, j] * us, q) for q in (10, 50, 90)} for j in range(frame_d.shape[1])},
@@ -88,6 +89,27 @@ def main():
         "xcc_waves": np.bincount(xcc & 0xF, minlength=8).tolist(),
         "distinct_cu_se_xcc": int(len(set(zip(cu.tolist(), se.tolist(), (xcc & 0xF).tolist())))),
     }
+    # placement: waves per SIMD, wave index -> SIMD, and whether workgroups k, k + 256,
+    # k + 512 share a CU (what a placement-aware run-length pattern would rely on)
+    simd = (hw >> 4) & 0x3
+    sh = (hw >> 12) & 0x1
+    cukey = (xcc & 0xF) * 4096 + se * 512 + sh * 256 + cu
+    simdkey = cukey * 4 + simd
+    _, per_simd = np.unique(simdkey, return_counts=True)
+    _, per_cu = np.unique(cukey, return_counts=True)
+    wave_in_wg = np.arange(len(st)) % 4
+    wg = np.arange(len(st)) // 4
+    res["placement"] = {
+        "simds_used": int(per_simd.size), "waves_per_simd_hist": np.bincount(per_simd).tolist(),
+        "cus_used": int(per_cu.size), "waves_per_cu_hist": np.bincount(per_cu).tolist(),
+        "wave_index_equals_simd_frac": float(np.mean(wave_in_wg == simd)),
+    }
+    cu_of_wg = {}
+    for i in range(len(st)):
+        cu_of_wg.setdefault(int(wg[i]), set()).add(int(cukey[i]))
+    pairs = [(k, k + 256) for k in range(len(cu_of_wg)) if k + 256 in cu_of_wg]
+    res["placement"]["wg_k_and_k256_same_cu_frac"] = float(np.mean([cu_of_wg[a] == cu_of_wg[b] for a, b in pairs])) if pairs else None
+    res["placement"]["wg_single_cu_frac"] = float(np.mean([len(v) == 1 for v in cu_of_wg.values()]))
     # time histogram of live waves (how many waves run at each microsecond of the launch)
     edges = np.arange(0, res["launch_span_us"] + 1.0, 1.0)
     live = [int(np.sum(((rt0 - t_min) * us <= e) & ((rt1 - t_min) * us > e))) for e in edges]

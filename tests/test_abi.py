@@ -112,16 +112,17 @@ def test_prefetch_kernels_have_no_spills():
     for name, info in rows.items():
         m = re.match(r"_ZN2pv14k_std_analysisILi(\d+)E", name)
         n = re.match(r"_ZN2pv11k_synthesisILi(\d+)ELi\dELi([124])E", name)
-        if (m and int(m.group(1)) <= 1024) or (n and int(n.group(1)) <= 512):
+        f = re.match(r"_ZN2pv7k_fusedILi512E", name)
+        if (m and int(m.group(1)) <= 1024) or (n and int(n.group(1)) <= 512) or f:
             checked += 1
             assert info.get("VGPRs Spill") == "0" and info.get("AGPRs") == "0", (name, info)
     assert checked >= 4 + 3 * 3 * 3
     # the occupancy the hot kernels are sized for (the config-2 single
-    # launch fits one round at 4 waves/SIMD, the analyses run at 3 or more, the config-4
-    # synthesis at the 2 its LDS allows)
+    # launch holds 3 workgroups per CU (balanced runs) at 3 waves/SIMD with no spills, the
+    # analyses run at 3 or more, the config-4 synthesis at the 2 its LDS allows)
     floors = {r"_ZN2pv11k_synthesisILi512ELi0ELi1ELb1ELb1": 3, r"_ZN2pv11k_synthesisILi1024ELi[02]ELi4ELb1": 2,
               r"_ZN2pv14k_std_analysisILi1024ELb0ELi[124]ELb1": 3,
-              r"_ZN2pv14k_std_analysisILi512ELb0ELi2ELb1": 3, r"_ZN2pv7k_fusedILi512ELi2ELi2E": 4}
+              r"_ZN2pv14k_std_analysisILi512ELb0ELi2ELb1": 3, r"_ZN2pv7k_fusedILi512ELi[23]ELi2E": 3}
     for pat, floor in floors.items():
         hits = [(n, i) for n, i in rows.items() if re.match(pat, n)]
         assert hits, pat

@@ -118,23 +118,52 @@ def test_fused_odd_output_stride_and_offset_input(cuda):
     assert torch.all(big[:, olen:] == 7.0)
 
 
-def test_fused_without_spectrum_output(cuda):
+@pytest.mark.parametrize("N,hop_div,effect,scale", [
+    (1024, 4, PITCH_SHIFT, 2.0),   # config 2: bins 257 .. 512 unread (a half-read pair)
+    (256, 2, PITCH_SHIFT, 3.0),    # L = 128: only bins 0 .. 42 read (one register)
+    (512, 4, PITCH_SHIFT, 2.0),    # L = 256
+    (1024, 4, TIME_SHIFT, 2.0),    # stretch: every bin read
+])
+def test_fused_without_spectrum_output(cuda, N, hop_div, effect, scale):
     """pv_process with spec = NULL on the single launch (SURVEY §8(d) fused mode: the rows
-    are consumed on chip): the same output bits as with the spectrum written; the split path
-    refuses a missing spectrum buffer."""
+    are consumed on chip, and for pitch > 1 the bins no output bin reads are not analysed):
+    the same output bits as with the spectrum written; the split path refuses a missing
+    spectrum buffer."""
     import torch
     from pvamd import _lib
     x = synth(44100 * 3, 31)
-    pv = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=600)
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_frames=1200)
     assert pv.single_launch
     out1, spec = pv.process(to_dev(x))
     out2, none = pv.process(to_dev(x), spectrum=False)
     assert none is None and spec is not None
     assert torch.equal(out1, out2)
-    ref = pvref.std_process(x, 1024, 4, ord("p"), 2.0)
+    ref = pvref.std_process(x, N, hop_div, ord(effect), scale)
     assert rms(out2.cpu().numpy()[0], ref) <= RMS_TOL
     split = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=600)
     assert not split.single_launch
     with pytest.raises(Exception):
         split.process(to_dev(x), spectrum=False)
     assert _lib.lib() is not None
+
+
+@pytest.mark.parametrize("seconds", [60.0, 20.0, 37.3])
+def test_fused_balanced_runs(cuda, monkeypatch, seconds):
+    """One long stream whose workgroups do not fill whole rounds of the CUs takes the
+    balanced single launch (some runs one frame longer, exactly `rounds` workgroups per CU):
+    every sample against the oracle, and within 1e-6 of the uniform-run launch
+    (PV_FUSED_BALANCE=0) — only the run seams' rounding moves."""
+    import torch
+    n = int(seconds * 44100)
+    x = synth(n, 20241)
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=pv_frames(n))
+    out, _ = pv.process(to_dev(x), spectrum=False)
+    g = out.cpu().numpy()[0]
+    ref = pvref.std_process(x, 1024, 4, ord("p"), 2.0)
+    assert g.shape == ref.shape and np.isfinite(g).all()
+    assert rms(g, ref) <= RMS_TOL
+    monkeypatch.setenv("PV_FUSED_BALANCE", "0")
+    out0, _ = pv.process(to_dev(x), spectrum=False)
+    assert float((out0 - out).abs().max()) <= 1e-6
+    again, _ = pv.process(to_dev(x), spectrum=False)  # deterministic
+    assert torch.equal(again, out0)
