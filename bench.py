@@ -183,8 +183,9 @@ def main():
                     help="skip the oracle check of the timed batch (profiling passes only)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--write-spec", action="store_true",
-                    help="c2 (single launch): also write the spectrum rows to HBM (by default the "
-                         "fused path keeps them on chip: SURVEY §8(d) fused mode)")
+                    help="hand the spectrum rows back to the caller (by default STANDARD runs do not: "
+                         "the single launch keeps them on chip, SURVEY §8(d) fused mode; the split "
+                         "path still round-trips every row through HBM)")
     ap.add_argument("--layout", choices=["packed", "natural"], default="packed",
                     help="STANDARD spectrum rows of the pv_process workspace (include/pv.h "
                          "pv_spec_layout): packed (default) folds the real bin N/2 into slot 0 "
@@ -289,10 +290,14 @@ def main():
     x_host = synth_channels_np(C, n, 20240 + rank * C, threads)
     x = torch.from_numpy(x_host).to(dev)
     t_gen = time.perf_counter() - t_gen
-    # the single launch (config 2) consumes the spectrum on chip unless --write-spec; the split
-    # path materialises it between its launches (the reference's caller-owned buffers)
-    spec_on_chip = bool(pv.single_launch) and not args.write_spec
-    spec = None if spec_on_chip else pv.alloc_spec(C, frames)
+    # STANDARD workloads do not hand the spectrum back (the reference's main.cpp never reads
+    # it) unless --write-spec: the single launch (config 2) then consumes it on chip, the
+    # split path still writes and re-reads every row (the handle's own buffer; for pitch > 1
+    # the bins no output bin reads are not analysed, zeros are stored in their slots).
+    # REF_COMPAT fills the caller's 2N-bin rows, as kernel.cu does.
+    want_spec = args.write_spec or compat
+    spec_on_chip = bool(pv.single_launch) and not want_spec
+    spec = pv.alloc_spec(C, frames) if want_spec else None
     out = pv.alloc_out(C, frames)
     stream = torch.cuda.current_stream(dev)
 
@@ -301,7 +306,7 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        pv.process(x, spec=spec, out=out, spectrum=not spec_on_chip)
+        pv.process(x, spec=spec, out=out, spectrum=want_spec)
     torch.cuda.synchronize(dev)
 
     # kernel durations for the roofline, on the launch stream (pv launches on torch's current
@@ -322,7 +327,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        pv.process(x, spec=spec, out=out, spectrum=not spec_on_chip)
+        pv.process(x, spec=spec, out=out, spectrum=want_spec)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
@@ -341,6 +346,16 @@ def main():
     value = total_frames / dt
 
     hop_a, hop_s, B = N // hop_div, pv.outHopSize, pv.spec_bins
+    # the row slots the analysis writes per frame: all of them, or — no spectrum handed back,
+    # pitch > 1, L = 1024 (config 4) — only the lane registers holding a bin some output bin
+    # reads (pv_analysis.hip NA instantiations: 64 NA slots).  The roofline counts those for
+    # both halves — the bytes the algorithm moves; the synthesis still loads whole rows (the
+    # stale slots are no output bin's source), so its traffic exceeds that
+    B_full = B
+    if not want_spec and not compat and not pv.single_launch and effect == PITCH_SHIFT and scale > 1.0 \
+            and N // 2 == 1024 and layout == PV_SPEC_PACKED and hop_a == 512:
+        src_hi = max(k for k in range(N // 2 + 1) if math.floor(scale * k + 0.5) <= N // 2)
+        B = min(B, 64 * 2 * ((src_hi + 128) // 128))
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     avg_ms = ms_tot / max(launches, 1)
@@ -417,8 +432,10 @@ def main():
             "config": {"workload": wl_desc,
                        "channels_per_gpu": C, "frames_per_channel": frames, "N": N, "hop": hop_a,
                        "out_hop": hop_s, "spec_layout": args.layout,
+                       "spec_slots_carried": B, "spec_slots": B_full,
                        "spectrum": "kept on chip (single launch, SURVEY §8(d) fused mode)" if spec_on_chip
-                                   else "written to HBM",
+                                   else ("returned to the caller" if want_spec else
+                                         "written to and re-read from HBM, not returned (the handle's own rows)"),
                        "parallelism": f"channel-shard x{world}",
                        "dist_backend": backend if distributed else None},
             "roofline": roof,

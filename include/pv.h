@@ -201,10 +201,13 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
                          int frames, const float* ola_in, long long ld_ola, float* out,
                          long long ldo, void* stream);
 
-/* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer).  When the
- * handle takes the single launch (pv_info.single_launch = 1), spec may be NULL: the spectrum
- * is then computed and consumed on chip and not written (SURVEY §8(d) fused mode); the split
- * path needs it (PV_ERR_ARG otherwise). */
+/* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer).  spec may
+ * be NULL when the caller does not want the spectrum: on the single launch (pv_info.
+ * single_launch = 1) it is then computed and consumed on chip and not written (SURVEY §8(d)
+ * fused mode); on the split path it goes through the handle's own buffer (max_channels x
+ * max_frames rows, allocated by the first such call: PV_ERR_NOMEM if that fails).  Either
+ * way, for pitch > 1 the bins no output bin reads (above about L / scale) may be left
+ * unanalysed; the output is the same bits as with a spectrum buffer. */
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);

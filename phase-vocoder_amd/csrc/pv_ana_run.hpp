@@ -62,7 +62,7 @@ constexpr int row_stores() { return PACKED ? E : E + 1; }
 // another launch, long after they would have left the caches).  rec (nullable): the run
 // record {S, phi(t0), phi(t0 + nfr - 1)} (kRecFields rows of bins_pad words, phases as their
 // float bits).
-template <int L, bool EKL, int D, bool PACKED, int RING = 0>
+template <int L, bool EKL, int D, bool PACKED, int RING = 0, int NA = Geo<L>::E>
 __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile, float* ring,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
                                         float e_lane, int* rec, float (&phprev)[Geo<L>::E + 1],
@@ -71,7 +71,9 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int CH = kAnaChunk;
-    constexpr int NST = row_stores<E, PACKED>();
+    // row stores per frame: every slot, or with NA < E the NA analysed ones (+ bin L's
+    // separate store in the natural layout, zeros)
+    constexpr int NST = (NA < E) ? (PACKED ? NA : NA + 1) : row_stores<E, PACKED>();
     // (PV_ABL_*: diagnostic timing-only ablations for A/B runs, wrong outputs: NOSTORE drops
     // the row stores (the magnitudes go to a sink so that they are still computed), NOATAN
     // the atan2, NOFFT the forward transform, NOWIN the window's LDS reads, L2IN the input's
@@ -111,6 +113,11 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             z[q].y = xr[q].y * wv.y;
         }
     };
+    // NA < E (pv_process without a spectrum output, pitch > 1: the launcher's instantiation
+    // for p.src_hi): only the lane registers p < NA (bins < 64 NA) are analysed, bin L only
+    // when NA = E.  Compile-time, so the frame has no data-dependent branch (a runtime one
+    // made the compiler copy in-flight prefetch registers: scripts/prefetch_hazards.py)
+    static_assert(NA % CH == 0 && NA >= CH && NA <= E, "whole chunks");
     auto frame = [&](int u, float2 (&z)[E]) {
         float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
         (void)srow;
@@ -121,7 +128,8 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         // bin L first (the packed slot 0 pairs it with bin 0): it is real, so its contract
         // phase is +0 or pi and needs no atan2 — computed once, wave-uniformly, instead of as
         // a ninth generic bin on every lane (bin_l_real)
-        float magL, phL;
+        float magL = 0.0f, phL = 0.0f;
+        if constexpr (NA == E) {
         bin_l_real<L, true>(z, twsl, magL, phL);
         // bin L's decision (wave-uniform; lane 0's copy is the one recorded).  Frame t0's
         // decision is against phprev = 0, not phi(t0 - 1): it is taken back out of S at once
@@ -135,10 +143,14 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             }
         }
         phprev[E] = phL;
+        }
         // bins 0 .. E-1 of the lane in chunks of CH (bounded live registers), all reads of a
         // chunk batched, phases of each pair through the packed atan2
         static_for<0, E / CH>([&](auto ic) {
             constexpr int p0 = decltype(ic)::value * CH;
+            // (chunks p0 >= NA: nothing — no bin of theirs is read, their row slots are not
+            // written, and NST counts the stores that are)
+            if constexpr (p0 >= NA) return;
             float2 X[CH];
             split_chunk_bp<L, CH, true, p0, false>(z, twsl, lane, X);
             float phs[CH];

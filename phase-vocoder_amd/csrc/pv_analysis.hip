@@ -40,7 +40,10 @@ constexpr int ana_ring() { return (D == 2 && L == 512) ? PV_ANA_RING : 0; }
 template <int L, int D>
 constexpr int ana_waves() { return (ana_ring<L, D>() > 0 || (PV_ANA_BIGWG && D == 2 && L == 512)) ? PV_ANA_WAVES : 4; }
 
-template <int L, bool EKL, int D, bool PACKED, int W = ana_waves<L, D>(), int RING = ana_ring<L, D>()>
+// NA: lane registers analysed (Geo<L>::E = all; fewer: bins >= 64 NA not analysed, zeros in
+// their row slots — pv_process without a spectrum output, ana_run)
+template <int L, bool EKL, int D, bool PACKED, int W = ana_waves<L, D>(), int RING = ana_ring<L, D>(),
+          int NA = Geo<L>::E>
 __global__ __launch_bounds__(64 * W, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(64 * W, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 :
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad : nullptr;
     float phprev[E + 1];
     ana_acc_t<L> sacc[E + 1];
-    ana_run<L, EKL, D, PACKED, RING>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, rings + w * RING * 128 * D,
+    ana_run<L, EKL, D, PACKED, RING, NA>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, rings + w * RING * 128 * D,
                                      tw0, lane, c, t0, nfr, e_lane, rec, phprev, sacc);
 }
 
@@ -274,7 +277,18 @@ static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hi
             };
             if (d == 1) go(k_std_analysis<LL, false, D1, PK>, ana_waves<LL, D1>(), ana_lds_std<LL, D1>(false));
             else if (d == 2) go(k_std_analysis<LL, false, D2, PK>, ana_waves<LL, D2>(), ana_lds_std<LL, D2>(false));
-            else go(k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
+            else if (LL == 1024 && PK && p.src_hi < LL) {
+                // bins above src_hi unread (config 4, pitch 1.5: 684 .. 1024): the registers
+                // analysed, in whole chunks of kAnaChunk
+                constexpr int W4 = ana_waves<LL, D4>(), R4 = ana_ring<LL, D4>();
+                const int na = kAnaChunk * ((p.src_hi + 64 * kAnaChunk) / (64 * kAnaChunk));
+                const size_t lds = ana_lds_std<LL, D4>(false);
+                if (na <= 8) go(k_std_analysis<LL, false, D4, PK, W4, R4, (8 < E_ ? 8 : E_)>, W4, lds);
+                else if (na <= 10) go(k_std_analysis<LL, false, D4, PK, W4, R4, (10 < E_ ? 10 : E_)>, W4, lds);
+                else if (na <= 12) go(k_std_analysis<LL, false, D4, PK, W4, R4, (12 < E_ ? 12 : E_)>, W4, lds);
+                else if (na <= 14) go(k_std_analysis<LL, false, D4, PK, W4, R4, (14 < E_ ? 14 : E_)>, W4, lds);
+                else go(k_std_analysis<LL, false, D4, PK>, W4, lds);
+            } else go(k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
         } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false, 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
         else hipLaunchKernelGGL((k_std_analysis<LL, true, 0, PK>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });

@@ -154,6 +154,9 @@ struct pv_handle {
     // workspace
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
+    // pv_process without a spectrum buffer on the split path: the handle's own rows
+    // (max_channels x max_frames, allocated at the first such call)
+    pv_float2* d_spec_own = nullptr;
     int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
 #ifdef PV_FUSED_STAMPS
     unsigned long long* d_stamps = nullptr;  // diagnostic build: per-wave phase stamps of k_fused
@@ -273,8 +276,11 @@ pv_status check_common(const pv_handle* h, int channels, int frames) {
     return PV_OK;
 }
 
+// src_hi < 0: every bin analysed (the spectrum is an output); otherwise the bins above it
+// may be left out (pv_process without a spectrum buffer: no output bin reads them)
 pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, int C, int frames,
-                      pv_float2* spec, long long ld_spec, bool want_runsum, hipStream_t s) {
+                      pv_float2* spec, long long ld_spec, bool want_runsum, hipStream_t s,
+                      int src_hi = -1) {
     if (C == 0 || frames == 0) return PV_OK;
     if (!x || !spec) return fail(PV_ERR_ARG, "null x/spec");
     if (ld_spec < (long long)frames * h->spec_stride)
@@ -301,6 +307,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.bins_pad = h->bins_pad;
     p.nan_faithful = h->nan_faithful;
     p.packed = h->packed;
+    p.src_hi = (src_hi < 0) ? h->L_ana : std::min(src_hi, h->L_ana);
     if (h->mode == PV_MODE_STANDARD)
         PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
     else
@@ -550,7 +557,7 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails, h->d_seam_flags};
+                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_spec_own};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 #ifdef PV_FUSED_STAMPS
@@ -869,11 +876,27 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     ProfCall pc_(h);
     hipStream_t s = (hipStream_t)stream;
     if (h->F_fused > 0) return do_fused(h, x, ldx, n_samples, channels, frames, spec, ld_spec, out, ldo, s);
-    if (!spec && channels > 0 && frames > 0)
-        return fail(PV_ERR_ARG, "null spec: the split path's spectrum buffer (only the single launch runs without one)");
+    // spec == NULL: the rows go through the handle's own buffer, and bins no output bin reads
+    // (pitch > 1) are not analysed
+    int src_hi = -1;
+    if (!spec && channels > 0 && frames > 0) {
+        if (!h->d_spec_own) {
+            const size_t bytes = sizeof(pv_float2) * (size_t)h->cfg.max_channels *
+                                 (size_t)h->cfg.max_frames * (size_t)h->spec_stride;
+            if (hipMalloc(&h->d_spec_own, bytes) != hipSuccess) {
+                h->d_spec_own = nullptr;
+                return fail(PV_ERR_NOMEM, "spectrum buffer of a spec = NULL call");
+            }
+        }
+        spec = h->d_spec_own;
+        ld_spec = (long long)h->cfg.max_frames * h->spec_stride;
+        if (h->mode == PV_MODE_STANDARD) src_hi = h->src_hi;
+    }
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
-    st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s);
+    st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s, src_hi);
     if (st != PV_OK) return st;
+    // (the synthesis reads whole rows: an instantiation reading only the analysed slots was
+    // 5 % slower on config 4, profiles/r05_ab_c4_skip.txt)
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
 }
 

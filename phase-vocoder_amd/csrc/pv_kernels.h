@@ -39,6 +39,9 @@ struct AnaParams {
     int bins_pad;
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
     int packed;             // STANDARD rows in the PV_SPEC_PACKED layout (bin L in slot 0)
+    int src_hi;             // STANDARD, L >= 1024: bins above it are not analysed (their row
+                            // slots get zeros) — pv_process without a spectrum output; L
+                            // otherwise
 };
 
 struct ScanParams {

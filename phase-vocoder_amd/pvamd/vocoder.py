@@ -202,8 +202,10 @@ class PhaseVocoder:
 
     def process(self, x, frames: int | None = None, n_samples: int | None = None, spec=None,
                 out=None, stream=None, spectrum: bool = True):
-        """analysis -> processing -> resynthesis; returns (out, spec).  spectrum=False (single
-        launch only, pv_info.single_launch): no spectrum is written, spec is None."""
+        """analysis -> processing -> resynthesis; returns (out, spec).  spectrum=False: the
+        caller gets no spectrum (spec is None) — the single launch keeps the rows on chip, the
+        split path uses the handle's own buffer; for pitch > 1 the bins no output bin reads
+        are then not analysed (same output bits)."""
         x = self._as2d(x)
         C, n = x.shape
         n_samples = n if n_samples is None else n_samples

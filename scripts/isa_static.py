@@ -30,7 +30,9 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
 KERNELS = {
     ("c3", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi512ELb0ELi2ELb1E", 9),
     ("c3", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi0ELi1ELb1ELb1E", 17),
-    ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1E", 17),
+    # config 4 (bench.py: no spectrum handed back, pitch 1.5): the instantiation analysing
+    # lane registers 0 .. 11 (bins < 768; 12 square roots, no bin L)
+    ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1ELi4ELi0ELi12E", 12),
     ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),

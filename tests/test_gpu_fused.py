@@ -127,8 +127,8 @@ def test_fused_odd_output_stride_and_offset_input(cuda):
 def test_fused_without_spectrum_output(cuda, N, hop_div, effect, scale):
     """pv_process with spec = NULL on the single launch (SURVEY §8(d) fused mode: the rows
     are consumed on chip, and for pitch > 1 the bins no output bin reads are not analysed):
-    the same output bits as with the spectrum written; the split path refuses a missing
-    spectrum buffer."""
+    the same output bits as with the spectrum written (the split path's form is
+    tests/test_gpu_parity.py test_split_path_without_spectrum_output)."""
     import torch
     from pvamd import _lib
     x = synth(44100 * 3, 31)
@@ -140,10 +140,6 @@ def test_fused_without_spectrum_output(cuda, N, hop_div, effect, scale):
     assert torch.equal(out1, out2)
     ref = pvref.std_process(x, N, hop_div, ord(effect), scale)
     assert rms(out2.cpu().numpy()[0], ref) <= RMS_TOL
-    split = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=600)
-    assert not split.single_launch
-    with pytest.raises(Exception):
-        split.process(to_dev(x), spectrum=False)
     assert _lib.lib() is not None
 
 

@@ -73,6 +73,50 @@ def test_std_process_multichannel(cuda):
         assert rms(g[c], ref[c]) <= RMS_TOL
 
 
+@pytest.mark.parametrize("N,hop_div,effect,scale,packed", [
+    (2048, 4, PITCH_SHIFT, 1.5, True),    # config 4 (packed rows, as bench.py): bins 684 ..
+    (2048, 4, PITCH_SHIFT, 1.5, False),   # 1024 unread (2 of 8 pairs and bin L skipped)
+    (2048, 8, PITCH_SHIFT, 3.0, False),   # bins above 341 unread
+    (2048, 4, PITCH_SHIFT, 0.75, False),  # pitch < 1: every bin read
+    (2048, 4, TIME_SHIFT, 0.5, False),    # stretch at L = 1024
+    (1024, 4, TIME_SHIFT, 0.5, True),     # config 3 (L = 512: no skip in the kernel)
+    (1024, 4, PITCH_SHIFT, 1.5, False),
+])
+def test_split_path_without_spectrum_output(cuda, N, hop_div, effect, scale, packed):
+    """pv_process(spec = NULL) on the split path: the rows go through the handle's own
+    buffer and, for pitch > 1, the bins no output bin reads are not analysed — the output is
+    the same bits as with a caller-owned spectrum, before and after, on 3 channels; a
+    spectrum requested afterwards is complete (every bin, bit-exact phases)."""
+    import torch
+    C, n = 3, 60000
+    xs = np.stack([synth(n, 410 + c) for c in range(C)])
+    xd = to_dev(xs)
+    frames = pv_frames(n, N // hop_div)
+    from pvamd import _lib
+    lay = _lib.PV_SPEC_PACKED if packed else _lib.PV_SPEC_NATURAL
+    pv = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=frames + 5,
+                      spec_layout=lay)
+    assert not pv.single_launch
+    out1, spec1 = pv.process(xd)
+    out2, none = pv.process(xd, spectrum=False)
+    assert none is None
+    assert torch.equal(out1, out2)
+    out3, spec3 = pv.process(xd)
+    assert torch.equal(out3, out1) and torch.equal(spec3, spec1)
+    if not packed:
+        _, ph = pvref.std_analysis(xs[1], N, N // hop_div, frames)
+        g = spec3.cpu().numpy()[1, :frames, :N // 2 + 1, 1]
+        assert np.array_equal(g.view(np.uint32), ph.view(np.uint32))
+    ref, _ = pvref.std_process_batch(xs, N, hop_div, ord(effect), scale)
+    g2 = out2.cpu().numpy()
+    for c in range(C):
+        assert g2[c].shape == ref[c].shape and rms(g2[c], ref[c]) <= RMS_TOL, f"ch{c}"
+
+
+def pv_frames(n, hop):
+    return max(1, -(-(n - hop) // hop))
+
+
 def test_split_equals_fused(cuda):
     N, hop_div = 1024, 4
     x = synth(40000, 3)
