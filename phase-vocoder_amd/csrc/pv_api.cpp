@@ -105,8 +105,9 @@ void fft_table(int L, std::vector<float2>& t, bool v3 = false) {
 
 // d_tw_syn: the synthesis-side L-point table (stage-major or v3, fft_table), then at L = 1024
 // the v3 pass table of the batched synthesis's inverse FFT (k_synthesis reads tw + L; the
-// real-time and fused kernels run the analysis transform from the first table too)
-int tw_syn_len(int L) { return L == 1024 ? 2 * L : L; }
+// real-time and fused kernels run the analysis transform from the first table too), at
+// L = 256, 512 the L/2-point table of the fused pitch-2 resynthesis (k_fused MODE 4, tw + L)
+int tw_syn_len(int L) { return L == 1024 ? 2 * L : (L >= 256 ? L + L / 2 : L); }
 
 void split_twiddles(int N, std::vector<float2>& t) {
     t.resize(N / 2 + 1);
@@ -370,7 +371,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.q = h->q;
     p.q_pow2 = h->q_pow2;
     p.inv_q = h->inv_q;
-    p.tw = h->d_tw_syn + (tw_syn_len(h->L_syn) - h->L_syn);  // L = 1024: the v3 pass table
+    p.tw = h->d_tw_syn + (h->L_syn == 1024 ? h->L_syn : 0);  // L = 1024: the v3 pass table
     p.tws = h->d_tws_syn;
     p.gain = h->d_gain;
     p.rot = (h->mode == PV_MODE_REF_COMPAT) ? h->N / 2 : 0;
@@ -434,6 +435,11 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     p.src_cnt = h->d_src_cnt;
     p.rho = h->rho;
     p.gain = h->d_gain;
+    // pitch 2: the periodic half-size resynthesis (k_fused MODE 4); PV_FUSED_HALF=0 keeps the
+    // MODE 3 gather and the full-size inverse FFT (tests compare the two)
+    p.tw_half = (tw_syn_len(h->L_syn) == h->L_syn + h->L_syn / 2) ? h->d_tw_syn + h->L_syn : nullptr;
+    if (const char* eh = std::getenv("PV_FUSED_HALF"))
+        if (eh[0] == '0') p.tw_half = nullptr;
     p.hs = h->hs;
     p.spec = reinterpret_cast<float2*>(spec);
     p.ld_spec = ld_spec;
@@ -723,10 +729,14 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     split_twiddles(2 * h->L_ana, t);
     if ((st = upload_tab(&h->d_tws_ana, t)) != PV_OK) return bail(st);
     fft_table(h->L_syn, t);
-    if (tw_syn_len(h->L_syn) > h->L_syn) {
+    if (h->L_syn == 1024) {
         std::vector<float2> t3;
         fft_table(h->L_syn, t3, true);
         t.insert(t.end(), t3.begin(), t3.end());
+    } else if (tw_syn_len(h->L_syn) > h->L_syn) {
+        std::vector<float2> th;
+        fft_table(h->L_syn / 2, th);
+        t.insert(t.end(), th.begin(), th.end());
     }
     if ((st = upload_tab(&h->d_tw_syn, t)) != PV_OK) return bail(st);
     split_twiddles(N, t);

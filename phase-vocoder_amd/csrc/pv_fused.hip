@@ -17,6 +17,11 @@
 // The per-frame arithmetic is k_std_analysis's (window, FFT, split, atan2, sqrt) and
 // k_synthesis's (synth_frame, register overlap-add, tails, seams) operation for operation,
 // so the spectrum and the output are bit-identical to the split path (tests/test_gpu_parity.py).
+// MODE 4 (pitch exactly 2, L >= 256): output bin k' = 2 s takes source bin s and the odd
+// output bins are empty, so the output frame is periodic with period N/2 — it is resynthesised
+// by an N/2-point inverse real FFT of bins 0 .. L/2 (the analysis registers 0 .. E/2, bin L/2
+// on lane 0 of register E/2, exactly the half-size transform's layout) and repeated: half the
+// inverse FFT, sin/cos and pre-step work, no gather (results within rounding of MODE 3).
 // Geometry as k_synthesis: a wave = a run of F frames of one channel, 4 runs per workgroup,
 // the intra-workgroup seams closed after one barrier, the inter-workgroup seams by the
 // second of the two workgroups to finish (no k_seam launch).
@@ -45,9 +50,6 @@ struct FuGeo {
     static_assert(O_SRC % 2 == 0 && O_TILE % 4 == 0, "alignment of the LDS carve-up");
 };
 
-// 4 waves per SIMD (<= 128 VGPRs): a single stream's runs (config 2: 3445 waves) then fit the
-// chip in one round (at 131 VGPRs, 3 per SIMD, a tenth of them ran as a second round:
-// config 2 fused 53.5-55.2 -> 45.2-46.2 us)
 template <int L, int MODE, int DT>
 // waves per SIMD k_fused is compiled for: 3 (<= 168 VGPRs; the balanced config-2 launch
 // holds exactly 3 workgroups per CU) — at 4 (<= 128) the L = 512 kernels spilled 6-12 VGPRs
@@ -79,6 +81,12 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
     float2* tiles = reinterpret_cast<float2*>(fsm + FG::O_TILE);
     float* winl = fsm + FG::O_WIN;
     int* srcl = reinterpret_cast<int*>(fsm + FG::O_SRC);
+    // MODE 4: the half-size transform's stage-major twiddles (L/2) and split twiddles
+    // e^{-2 pi i k/(N/2)}, k <= L/2, in the pitch map's area (2L + 2 <= 2B + 2 floats)
+    static_assert(MODE != 4 || L >= 256, "half-size synthesis: L/2 >= 128");
+    constexpr int LH = (MODE == 4) ? L / 2 : L;
+    float2* twl_h = reinterpret_cast<float2*>(fsm + FG::O_SRC);
+    float2* twsl_h = twl_h + LH;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR arithmetic
@@ -168,13 +176,24 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
     // tables -> LDS: every load issued before the first LDS write, so the set-up costs one
     // round trip instead of one per loop trip (config 2 stamps: 2.6 us of a 27.6 us wave)
     float2 tw0[E];
+    float2 tw0h[Geo<LH>::E];  // MODE 4: the half-size inverse transform's first-pass twiddles
     float2 gn[NS];  // synthesis gains of the lane's OLA slots (frame-invariant)
     {
         constexpr int KT = (L + 255) / 256, KB = (B + 255) / 256, KW = N / 256;
+        constexpr int KTH = (LH + 255) / 256, KSH = (LH + 1 + 255) / 256;
         static_assert(N % 256 == 0, "window in whole 256-thread trips");
-        float2 ttw[KT], tts[KB];
+        float2 ttw[KT], tts[KB], tth[KTH], tsh[KSH];
         int tsf[KB], tsc[KB];
         float twn[KW];
+        if constexpr (MODE == 4) {
+#pragma unroll
+            for (int k = 0; k < KTH; ++k)
+                if (tid + 256 * k < LH) tth[k] = p.tw_half[tid + 256 * k];
+#pragma unroll
+            for (int k = 0; k < KSH; ++k)
+                if (tid + 256 * k <= LH) tsh[k] = p.tws[2 * (tid + 256 * k)];
+            load_tw0<LH>(tw0h, p.tw_half);
+        }
 #pragma unroll
         for (int k = 0; k < KT; ++k)
             if (tid + 256 * k < L) ttw[k] = p.tw[tid + 256 * k];
@@ -205,6 +224,14 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
                 // MODE 3 (pitch >= 1): the source's byte offset in a wave's tile, zero slot L + 1
                 if (MODE == 3) srcl[i] = (int)sizeof(float2) * (tsf[k] >= 0 ? tsf[k] : L + 1);
             }
+        }
+        if constexpr (MODE == 4) {
+#pragma unroll
+            for (int k = 0; k < KTH; ++k)
+                if (tid + 256 * k < LH) twl_h[tid + 256 * k] = tth[k];
+#pragma unroll
+            for (int k = 0; k < KSH; ++k)
+                if (tid + 256 * k <= LH) twsl_h[tid + 256 * k] = tsh[k];
         }
 #pragma unroll
         for (int k = 0; k < KW; ++k) winl[tid + 256 * k] = twn[k];
@@ -298,6 +325,29 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
             }
             wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers
+            if constexpr (MODE == 4) {
+                // bins 0 .. L/2 - 1 are registers 0 .. EH - 1, bin L/2 is lane 0 of register
+                // EH: the half-size transform's own layout
+                constexpr int EH = Geo<LH>::E;
+                float2 svh[EH + 1], zh[EH];
+                int Mh[EH + 1];
+                float phh[EH + 1], ekh[EH + 1];
+                unsigned jkh[EH + 1];
+#pragma unroll
+                for (int i = 0; i <= EH; ++i) svh[i] = sv[i];
+                const SynLds stbh{twl_h, twsl_h, nullptr, nullptr, nullptr};
+                synth_frame<LH, 0, false, true, false, false, true>(svh, false, 0u, Mh, phh, pmap, stbh, tw0h,
+                                                                    tile, lane, zh, ekh, jkh);
+                // y[n] = y_half[n mod N/2]: slot s of the frame is the half frame's slot s mod EH
+                float2 zs[EH];
+#pragma unroll
+                for (int idx = 0; idx < EH; ++idx) zs[last_slot<LH>(idx)] = zh[idx];
+#pragma unroll
+                for (int cs = 0; cs < E; ++cs) {
+                    acc[cs].x = __builtin_fmaf(zs[cs % EH].x, gn[cs].x, acc[cs].x);
+                    acc[cs].y = __builtin_fmaf(zs[cs % EH].y, gn[cs].y, acc[cs].y);
+                }
+            } else {
             synth_frame<L, MODE, false, true, false, false, true>(sv, false, 0u, M, phprev, pmap, stb, tw0, tile,
                                                                   lane, z, ekr, jkr);
             // ---- windowed overlap-add in registers
@@ -306,6 +356,7 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
                 const int cs = last_slot<L>(idx);
                 acc[cs].x = __builtin_fmaf(z[idx].x, gn[cs].x, acc[cs].x);
                 acc[cs].y = __builtin_fmaf(z[idx].y, gn[cs].y, acc[cs].y);
+            }
             }
         }
         // positions [u*hs, (u+1)*hs) = slots 0..D-1 are final — except a workgroup's head
@@ -401,6 +452,11 @@ static hipError_t launch_fused_m(int L, int dt, dim3 grid, const FusedParams& p,
 hipError_t launch_fused(int L, int mode, int channels, const FusedParams& p, hipStream_t s) {
     const dim3 grid(p.nwg, channels);
     const int dt = p.hs / 128;
+    // pitch exactly 2: the periodic half-size resynthesis (MODE 4)
+    if (mode == 2 && p.rho == 2.0f && p.tw_half != nullptr) {
+        if (L == 256) return launch_fused_l<256, 4>(dt, grid, p, s);
+        if (L == 512) return launch_fused_l<512, 4>(dt, grid, p, s);
+    }
     if (mode == 2 && p.rho >= 1.0f) return launch_fused_m<3>(L, dt, grid, p, s);
     return mode == 2 ? launch_fused_m<2>(L, dt, grid, p, s) : launch_fused_m<0>(L, dt, grid, p, s);
 }

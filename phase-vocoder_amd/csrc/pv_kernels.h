@@ -95,6 +95,7 @@ struct FusedParams {
     const int* src_cnt;
     float rho;
     const float* gain;                 // synthesis window * norm / N   (N)
+    const float2* tw_half;             // stage-major L/2-point table (pitch 2: MODE 4) or nullptr
     int hs;                            // out hop
     float2* spec;
     long long ld_spec;

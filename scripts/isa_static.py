@@ -36,8 +36,9 @@ KERNELS = {
     ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
-    # config 2's single launch: analysis + synthesis of a frame in one loop trip (9 + 17)
-    ("c2", "fused"): ("pv_fused.hip", [], "_ZN2pv7k_fusedILi512ELi3ELi2EE", 26),
+    # config 2's single launch (pitch 2: MODE 4, the half-size resynthesis): analysis +
+    # synthesis of a frame in one loop trip (9 square roots + 5 cosines and 5 sines)
+    ("c2", "fused"): ("pv_fused.hip", [], "_ZN2pv7k_fusedILi512ELi4ELi2EE", 19),
     # config 5's per-callback kernel: one frame per wave and launch, no frame loop — the whole
     # kernel is priced (table staging included, its loops counted once); L = 128: 3 + 5
     ("rt", "rt"): ("pv_rt.hip", [], "_ZN2pv4k_rtILi128ELi2ELb1EE", None),

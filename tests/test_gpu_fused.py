@@ -75,10 +75,17 @@ def test_fused_equals_split_path(cuda, monkeypatch, N, hop_div, effect, scale):
     ref, _ = pvref.std_process_batch(xs, N, hop_div, ord(effect), scale)
     for c in range(C):
         assert rms(gf[c], ref[c]) <= RMS_TOL, f"ch{c}"
-    # same run length as the split path: bit for bit
+    # same run length as the split path: bit for bit — for pitch 2 at N >= 512 through the
+    # single launch's MODE 3 gather (PV_FUSED_HALF=0); its default half-size resynthesis
+    # (MODE 4) is the same sum with other roundings: within 1e-6
     monkeypatch.setenv("PV_FUSED_FRAMES", str(ps.frames_per_run))
+    half = effect == PITCH_SHIFT and scale == 2.0 and N >= 512
     pe = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=frames)
     out_e, _, _ = _kernels(pe, xd)
+    if half:
+        assert np.abs(out_e.cpu().numpy() - gs).max() <= 1e-6
+        monkeypatch.setenv("PV_FUSED_HALF", "0")
+        out_e, _, _ = _kernels(pe, xd)
     assert np.array_equal(out_e.cpu().numpy().view(np.uint32), gs.view(np.uint32))
 
 
