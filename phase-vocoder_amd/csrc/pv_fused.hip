@@ -10,13 +10,15 @@
 // frame, no run records and no second pass over the spectrum.  The spectrum row is still
 // stored (the caller's spectrum buffer is an output of pv_process), but it is
 // never read back: per frame 4 hop_a + 8 (N/2+1) + 4 hop_s bytes instead of the split
-// path's 4 hop_a + 16 (N/2+1) + 4 hop_s, and one launch instead of two.  Config 2, a
-// single stream, runs as one round of 3445 waves that is bound by the issue of the SIMDs
-// holding 4 of them, not by bytes (per-wave stamps).
+// path's 4 hop_a + 16 (N/2+1) + 4 hop_s, and one launch instead of two (with spec = NULL
+// the rows are not stored at all).  Config 2, a single stream, runs as exactly 3 workgroups
+// per CU (balanced runs, below), bound by the shared issue of the 3 waves per SIMD, not by
+// bytes (per-wave stamps).
 //
 // The per-frame arithmetic is k_std_analysis's (window, FFT, split, atan2, sqrt) and
 // k_synthesis's (synth_frame, register overlap-add, tails, seams) operation for operation,
-// so the spectrum and the output are bit-identical to the split path (tests/test_gpu_parity.py).
+// so the spectrum and the output are bit-identical to the split path (tests/test_gpu_fused.py)
+// — except MODE 4, whose output is the same sum rounded differently (within 1e-6).
 // MODE 4 (pitch exactly 2, L >= 256): output bin k' = 2 s takes source bin s and the odd
 // output bins are empty, so the output frame is periodic with period N/2 — it is resynthesised
 // by an N/2-point inverse real FFT of bins 0 .. L/2 (the analysis registers 0 .. E/2, bin L/2
