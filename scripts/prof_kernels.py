@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--calib", action="store_true")
     ap.add_argument("--layout", choices=["packed", "natural"], default="packed")
     ap.add_argument("--n", type=int, default=441000, help="samples per channel (c2: 2646000)")
+    ap.add_argument("--write-spec", action="store_true",
+                    help="hand the spectrum back (bench.py's --write-spec); by default STANDARD "
+                         "runs as bench.py does, without (REF_COMPAT always writes the caller's rows)")
     args = ap.parse_args()
     import torch
     from bench import synth_channels_np
@@ -34,10 +37,11 @@ def main():
     # host-generated input + plain copy: no torch compute kernels in the profiled process
     x = torch.from_numpy(synth_channels_np(args.channels, n, 20240)).to("cuda:0")
     frames = pv.num_frames(n)
-    spec = pv.alloc_spec(args.channels, frames)
+    want = args.write_spec or args.mode != "standard"
+    spec = pv.alloc_spec(args.channels, frames) if want else None
     out = pv.alloc_out(args.channels, frames)
     for _ in range(args.reps):
-        pv.process(x, spec=spec, out=out)
+        pv.process(x, spec=spec, out=out, spectrum=want)
     torch.cuda.synchronize()
     if args.calib:
         # traffic calibration: the batched FFT reads and writes exactly 8*n*batch bytes with

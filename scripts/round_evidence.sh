@@ -34,10 +34,11 @@ for s in $STEPS; do
     prof_c4) prof prof_c4 400 --workload c4 --steps 40 --warmup 3 --no-cpu ;;
     prof_compat) prof prof_compat 400 --workload compat --steps 20 --warmup 3 --no-cpu ;;
     prof_c2) prof prof_c2 400 --workload c2 --no-cpu ;;
-    traffic_c3|traffic_c4)
+    traffic_c3|traffic_c4|traffic_c2)
       w=${s#traffic_}; rm -rf gpurun_out/pmc
       args="--calib"; [ $w = c4 ] && args="--calib --N 2048 --effect p --scale 1.5"
-      PMC_SETS=scripts/pmc_sets_traffic.txt PROF_ARGS="$args" timeout -k 10 400 bash scripts/pmc_session.sh > gpurun_out/pmc_$w.log 2>&1
+      [ $w = c2 ] && args="--calib --channels 1 --n 2646000 --effect p --scale 2.0 --reps 20"
+      PV_TRAFFIC_WORKLOAD=$w PMC_SETS=scripts/pmc_sets_traffic.txt PROF_ARGS="$args" timeout -k 10 400 bash scripts/pmc_session.sh > gpurun_out/pmc_$w.log 2>&1
       rc=$?; tail -3 gpurun_out/pmc_$w.log; [ $rc -ne 0 ] && exit $rc
       rm -rf gpurun_out/pmc_$w && mv gpurun_out/pmc gpurun_out/pmc_$w ;;
     pmc)

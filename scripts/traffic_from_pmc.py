@@ -22,7 +22,7 @@ out = sys.argv[2] if len(sys.argv) > 2 else "profiles/traffic.json"
 CALIB_BYTES = 8 * 512 * 131072
 NAMES = {"k_std_analysis": "analysis", "k_synthesis": "synthesis", "k_carry": "carry",
          "k_seam": "seam", "k_runsum": "runsum", "k_compat_analysis": "compat_analysis",
-         "k_fft": "fft"}
+         "k_fft": "fft", "k_fused": "fused"}
 
 per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> dispatch
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
