@@ -68,6 +68,10 @@ template <int L, int MODE, int DT>
 #ifndef PV_FUSED_SKIP_UNREAD
 #define PV_FUSED_SKIP_UNREAD 1
 #endif
+// 0: every frame's samples loaded whole (A/B of the shifted-register input; same results)
+#ifndef PV_FUSED_SHIFT
+#define PV_FUSED_SHIFT 1
+#endif
 __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
     using G_ = Geo<L>;
     using FG = FuGeo<L>;
@@ -156,6 +160,22 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
     // input frame t: samples t*hop + 2 (lane + 64 q) + {0,1}; frames whose N samples are all
     // inside [0, n) use vector loads, the last N/hop of a channel the bounds-checked path
     const long long lastfull = (p.aligned && p.n >= N) ? (p.n - N) / p.hop : -1;
+    // registers E - DT .. E - 1 of frame t (its last 128 DT new sample pairs per lane)
+    auto load_tail = [&](int t, float2 (&xr)[E]) {
+        const long long base = (long long)t * p.hop;
+        if (t <= lastfull) {
+#pragma unroll
+            for (int q = E - DT; q < E; ++q) xr[q] = *reinterpret_cast<const float2*>(xc + base + 2 * (lane + 64 * q));
+        } else {
+#pragma unroll
+            for (int q = E - DT; q < E; ++q) {
+                const long long s = base + 2 * (lane + 64 * q);
+                xr[q].x = (s < p.n) ? xc[s] : 0.0f;
+                xr[q].y = (s + 1 < p.n) ? xc[s + 1] : 0.0f;
+            }
+        }
+    };
+    const bool shift_in = PV_FUSED_SHIFT && p.hop == 128 * DT;  // pitch: analysis hop = out hop
     auto load = [&](int t, float2 (&xr)[E]) {
         const long long base = (long long)t * p.hop;
         if (t <= lastfull) {
@@ -255,7 +275,22 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
                 }
             }
             if (u == 0) PV_STAMP(10);  // frame 0's samples have landed (F <= 7)
-            if (u + 1 < nfr) load(t + 1, xr);  // next frame's samples fly during this frame
+            // next frame's samples fly during this frame.  Pitch (analysis hop = out hop =
+            // 128 DT): frame t+1's register q is frame t's register q + DT, so only its DT
+            // new pairs per lane are loaded (as k_std_analysis's shifted-register input)
+            if (u + 1 < nfr) {
+                if constexpr (MODE >= 2 && DT < E) {
+                    if (shift_in) {
+#pragma unroll
+                        for (int q = 0; q + DT < E; ++q) xr[q] = xr[q + DT];
+                        load_tail(t + 1, xr);
+                    } else {
+                        load(t + 1, xr);
+                    }
+                } else {
+                    load(t + 1, xr);
+                }
+            }
             // ---- analysis (k_std_analysis's operations): spectrum row out, kept in sv.  The
             // split takes the partner bins from the last pass's registers by a lane reversal
             // (split_chunk_bp; bit-identical to the LDS-image split)
