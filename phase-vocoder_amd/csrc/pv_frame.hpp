@@ -225,7 +225,8 @@ struct SynLds {
 // 64 i, i < E, and k = L on lane 0).  MODE 0/2 STANDARD stretch/pitch (MODE 3: pitch with
 // at most one source per bin — ratio >= 1 — fixed at compile time) (unwrap state M,
 // phprev updated; add_decision = false for a run's first frame, whose decision the carry
-// already holds), MODE 1 REF_COMPAT (kernel.cu:121-129 y-bug).  tq = (t + 1) mod q.
+// already holds), MODE 1 REF_COMPAT (kernel.cu:121-129 y-bug), MODE 5: sv is the output
+// spectrum Y itself (k_fused MODE 4).  tq = (t + 1) mod q.
 // Result: STORE_LAST: time samples in tile (natural order, padded); else the inverse
 // FFT's last-pass registers z (point lane + 64 last_slot(idx)).
 // QPOW2: the output-phase denominator q is a power of two <= 2^24 (compile-time path);
@@ -278,7 +279,15 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
     float mag[E + 1], ph[E + 1];
     PV_FOR_BINS(E, lane, { mag[i] = sv[i].x; ph[i] = sv[i].y; })
     float2 Yr[E + 1];  // Y of the lane's bins k = lane + 64 i (+ bin L on lane 0)
-    if constexpr (MODE != 1) {
+    if constexpr (MODE == 5) {
+        // sv is Y itself (k_fused MODE 4's X^2 / |X|): no phase propagation
+        (void)mag; (void)ph;
+        PV_FOR_BINS(E, lane, {
+            float2 y = sv[i];
+            if (k == 0 || k == L) y.y = 0.0f;  // C2R ignores Im of DC and Nyquist
+            Yr[i] = y;
+        })
+    } else if constexpr (MODE != 1) {
         float phc[E + 1];
         float ekv[E + 1];
         unsigned jkv[E + 1];

@@ -23,7 +23,10 @@
 // output bins are empty, so the output frame is periodic with period N/2 — it is resynthesised
 // by an N/2-point inverse real FFT of bins 0 .. L/2 (the analysis registers 0 .. E/2, bin L/2
 // on lane 0 of register E/2, exactly the half-size transform's layout) and repeated: half the
-// inverse FFT, sin/cos and pre-step work, no gather (results within rounding of MODE 3).
+// inverse FFT and pre-step work, no gather; and since q = 1 makes the output phase exactly
+// 2 phi, its input Y_s = |X_s| e^{2 i phi_s} = X_s^2 / |X_s| comes from the split's X without
+// atan2 or sin/cos (the contract phases are computed only for a spectrum output).  Results
+// within rounding of MODE 3.
 // Geometry as k_synthesis: a wave = a run of F frames of one channel, 4 runs per workgroup,
 // the intra-workgroup seams closed after one barrier, the inter-workgroup seams by the
 // second of the two workgroups to finish (no k_seam launch).
@@ -300,6 +303,9 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
             fft_run<L, false, true>(z, tile, twl, tw0, lane);
 #endif
             float2 sv[E + 1];
+            // MODE 4: the half-size transform's input Y_s = |X_s| e^{2 i phi_s} = X_s^2 / |X_s|
+            // (q = 1: the output phase is exactly 2 phi), bins s <= L/2 — no atan2, no sin/cos
+            float2 yh[Geo<LH>::E + 1];
             float2* srow = specc + (long long)t * p.spec_stride + lane;
             // without a spectrum output only the bin pairs holding a bin some output bin reads
             // are analysed (pitch 2.0: bins 0 .. 256 of 512, so 3 of 4 pairs and no bin L): a
@@ -334,6 +340,20 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
 #else
                 split_chunk<L, CH, true>(tile, twsl, lane, i0, X);
 #endif
+                if constexpr (MODE == 4) {
+                    static_for<0, CH>([&](auto cc) {
+                        constexpr int i = i0 + decltype(cc)::value;
+                        if constexpr (i <= Geo<LH>::E) {
+                            // X came out doubled (TWICE): Y = X2^2 / (2 |X2|); |X| = 0 -> 0
+                            const float2 x2 = X[decltype(cc)::value];
+                            const float r = __builtin_fmaf(x2.x, x2.x, x2.y * x2.y);
+                            const float rs = (r > 0.0f) ? __builtin_amdgcn_rsqf(r) : 0.0f;
+                            yh[i] = make_float2(0.5f * __builtin_fmaf(x2.x, x2.x, -(x2.y * x2.y)) * rs,
+                                                x2.x * x2.y * rs);
+                        }
+                    });
+                    if (!wspec) return;  // no row to write: no phase, no magnitude
+                }
                 float phs[CH];
                 {
                     const f2v ph2 = atan2_pv2(X[0].y, X[0].x, X[1].y, X[1].x);
@@ -353,12 +373,12 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
                     }
                 });
             });
-            {
+            if (wspec) {
                 // slot 0: PV_SPEC_PACKED lane 0 carries bins 0 and L (both real)
                 const bool pk0 = p.packed && lane == 0;
                 const f2v s0 = pk0 ? f2v{pack_real_bin(sv[0].x, sv[0].y), pack_real_bin(sv[E].x, sv[E].y)}
                                    : f2v{sv[0].x, sv[0].y};
-                if (wspec) __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+                __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
             }
             wave_lds_sync();
             // ---- processing + resynthesis: inverse FFT's last-pass registers
@@ -371,9 +391,9 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
                 float phh[EH + 1], ekh[EH + 1];
                 unsigned jkh[EH + 1];
 #pragma unroll
-                for (int i = 0; i <= EH; ++i) svh[i] = sv[i];
+                for (int i = 0; i <= EH; ++i) svh[i] = yh[i];
                 const SynLds stbh{twl_h, twsl_h, nullptr, nullptr, nullptr};
-                synth_frame<LH, 0, false, true, false, false, true>(svh, false, 0u, Mh, phh, pmap, stbh, tw0h,
+                synth_frame<LH, 5, false, true, false, false, true>(svh, false, 0u, Mh, phh, pmap, stbh, tw0h,
                                                                     tile, lane, zh, ekh, jkh);
                 // y[n] = y_half[n mod N/2]: slot s of the frame is the half frame's slot s mod EH
                 float2 zs[EH];
