@@ -8,7 +8,11 @@
 //     the phase-vocoder kernels (fft_run, pv_device.hpp): the same radix-2 butterflies
 //     with table twiddles, log2(N/64) stages per register pass, an LDS exchange per pass.
 //   N = 2048: the same passes over two waves per transform (k_fft2w).
-//   N in [2, 64]: one transform per LANE, every stage in registers (k_fft_reg); the
+//   N = 32, 64 (round 5): T = N/8 lanes per transform, 8 points per lane — a radix-8 DIF
+//     in each lane over its points t + T p, the W_N^{t k1} twiddles, an 8 x T transpose
+//     through LDS within the wave, T-point DIFs, and T-lane-contiguous loads and stores
+//     (k_fft_t8: the one-transform-per-lane form needs 2N VGPRs and strided accesses);
+//   N in [2, 16]: one transform per LANE, every stage in registers (k_fft_reg); the
 //     per-stage LDS form (the reference's FftIteration in LDS, one transform per wave)
 //     remains for buffers that are not 16-byte aligned.
 // Unnormalised in both directions, like the reference (GPU_FFT applies no 1/N).
@@ -141,6 +145,71 @@ __global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, 
     }
 }
 
+
+// N = 8 T (T = 4, 8): T lanes per transform, 8 points per lane, 64 / T transforms per wave.
+// x[t + T p] -> lane t, point p.  X[k1 + 8 k2] = sum_t W_T^{t k2} W_N^{t k1} (sum_p W_8^{p k1}
+// x[t + T p]): the inner 8-point DFT in the lane (dif_v3<8>: output bit-reversed), the
+// twiddle (table tw of the radix-2 stages: W_N^e = tw[N/2 - 1 + e] for e < N/2, its negative
+// above), the transpose through LDS (rows of T + 1 float2, wave-local: no barrier), and
+// 8 / T T-point DFTs per lane (columns k1 = t + T j).  Unnormalised, conj twiddles for INV.
+template <int N, bool INV>
+__global__ __launch_bounds__(256) void k_fft_t8(const float2* __restrict__ in, float2* out,
+                                                const float2* __restrict__ tw, int batch) {
+    constexpr int T = N / 8, P = 8, NT = 256 / T, ROW = T + 1, J = P / T;
+    static_assert(T == 4 || T == 8, "N = 32 or 64");
+    __shared__ float2 xs[NT * P * ROW];
+    __shared__ float2 twl[N / 2];
+    const int tid = threadIdx.x;
+    const int g = tid / T, t = tid % T;
+    const long long b = (long long)blockIdx.x * NT + g;
+    const bool live = b < batch;
+    if (tid < N / 2) twl[tid] = tw[N / 2 - 1 + tid];
+    f2v a[P];
+    if (live) {
+        const float2* src = in + b * N + t;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const float2 v = src[T * p];
+            a[p] = f2v{v.x, v.y};
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) a[p] = f2v{0.0f, 0.0f};
+    }
+    __syncthreads();  // twl
+    dif_v3<P, INV>(a);  // a[bitrev3(k1)] = inner DFT k1
+    float2* row = xs + g * P * ROW;
+#pragma unroll
+    for (int k1 = 0; k1 < P; ++k1) {
+        f2v v = a[bitrevc(k1, 3)];
+        if (k1 > 0) {
+            const int e = t * k1;  // < N
+            const float2 w = lds_ld(&twl[e & (N / 2 - 1)]);
+            const f2v wv = (e & (N / 2)) ? f2v{-w.x, -w.y} : f2v{w.x, w.y};
+            v = cmul_v<INV>(v, wv);
+        }
+        row[k1 * ROW + t] = make_float2(v.x, v.y);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int k1 = t + T * j;
+        f2v c[T];
+#pragma unroll
+        for (int s2 = 0; s2 < T; ++s2) {
+            const float2 v = lds_ld(&row[k1 * ROW + s2]);
+            c[s2] = f2v{v.x, v.y};
+        }
+        dif_v3<T, INV>(c);  // c[bitrev(k2)] = X[k1 + 8 k2]
+        if (live) {
+#pragma unroll
+            for (int k2 = 0; k2 < T; ++k2) {
+                const f2v v = c[bitrevc(k2, ilog2c(T))];
+                out[b * N + k1 + P * k2] = make_float2(v.x, v.y);
+            }
+        }
+    }
+}
 
 // N = 2048: two waves per transform (128 "lanes" x E = 16 points: the register budget of the
 // N = 1024 kernel, which one wave holding 32 points per lane does not have — that form ran
@@ -300,6 +369,18 @@ hipError_t launch_fft(int n, int inverse, const float2* in, float2* out, const f
             const size_t lds = sizeof(float2) * (256 + 2 * kF2Tile);
             if (inverse) hipLaunchKernelGGL((k_fft2w<true>), g2, block, lds, s, in, out, tw, batch);
             else hipLaunchKernelGGL((k_fft2w<false>), g2, block, lds, s, in, out, tw, batch);
+            break;
+        }
+        case 32:
+        case 64: {
+            const dim3 g8((unsigned)((batch + 256 / (n / 8) - 1) / (256 / (n / 8))));
+            if (n == 32) {
+                if (inverse) hipLaunchKernelGGL((k_fft_t8<32, true>), g8, block, 0, s, in, out, tw, batch);
+                else hipLaunchKernelGGL((k_fft_t8<32, false>), g8, block, 0, s, in, out, tw, batch);
+            } else {
+                if (inverse) hipLaunchKernelGGL((k_fft_t8<64, true>), g8, block, 0, s, in, out, tw, batch);
+                else hipLaunchKernelGGL((k_fft_t8<64, false>), g8, block, 0, s, in, out, tw, batch);
+            }
             break;
         }
         default: {
