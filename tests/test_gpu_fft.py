@@ -42,13 +42,35 @@ def test_fft_in_place_and_roundtrip(cuda):
     import torch
     from pvamd.fft import fft
     rng = np.random.default_rng(3)
-    for n in (16, 512, 2048):
+    for n in (16, 32, 64, 512, 2048):
         x = (rng.standard_normal((9, n)) + 1j * rng.standard_normal((9, n))).astype(np.complex64)
         d = torch.from_numpy(x).cuda()
         fft(d, out=d)                # in place
         fft(d, inverse=True, out=d)  # unnormalised inverse: n * x
         back = d.cpu().numpy() / n
         assert rel_err(back, x) <= 2 * tol(n)
+
+
+@pytest.mark.parametrize("n", [16, 32, 64])
+def test_fft_small_n_offset_buffers_and_ragged_batch(cuda, n):
+    """n <= 64 on buffers only 8-byte aligned (one complex element past a 16-byte boundary)
+    and batches that leave a workgroup partly empty (k_fft_t8: 256 / (n / 8) transforms per
+    workgroup): every transform against the oracle, nothing written past the batch."""
+    import torch
+    from pvamd.fft import fft
+    rng = np.random.default_rng(100 + n)
+    for B in (1, 33, 67):
+        x = (rng.standard_normal((B, n)) + 1j * rng.standard_normal((B, n))).astype(np.complex64)
+        big = torch.zeros(B * n + 2, dtype=torch.complex64, device="cuda")
+        big[1:1 + B * n] = torch.from_numpy(x.reshape(-1)).cuda()
+        src = big[1:1 + B * n].view(B, n)
+        outb = torch.full((B * n + 2,), 7.0 + 0j, dtype=torch.complex64, device="cuda")
+        dst = outb[1:1 + B * n].view(B, n)
+        fft(src, out=dst)
+        g = dst.cpu().numpy()
+        for b in range(B):
+            assert rel_err(g[b], pvref.fft_c64(x[b])) <= tol(n), (n, B, b)
+        assert complex(outb[0].item()) == 7.0 + 0j and complex(outb[-1].item()) == 7.0 + 0j
 
 
 @pytest.mark.parametrize("name", ["50Hz", "50Hz+500Hz", "500Hz+505Hz+12000Hz"])
