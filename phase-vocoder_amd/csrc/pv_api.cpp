@@ -309,6 +309,19 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     p.nan_faithful = h->nan_faithful;
     p.packed = h->packed;
     p.src_hi = (src_hi < 0) ? h->L_ana : std::min(src_hi, h->L_ana);
+    if (h->mode == PV_MODE_REF_COMPAT) {
+        // the REF_COMPAT analysis has no run records: its runs only set which rows a wave
+        // writes in turn, and short runs (fewer rows written concurrently per channel, more
+        // channels' rows in address order) stream faster (profiles/r05_ab_compat_F.txt);
+        // the synthesis keeps h->F (its seams)
+        int fa = 4;
+        if (const char* ev = std::getenv("PV_COMPAT_ANA_FRAMES")) {
+            const int f = std::atoi(ev);
+            if (f >= 1 && f <= 256) fa = f;
+        }
+        p.F = fa;
+        p.nruns = (frames + fa - 1) / fa;
+    }
     if (h->mode == PV_MODE_STANDARD)
         PV_LAUNCH(h, KA, s, pv::launch_std_analysis(h->L_ana, C, p, s));
     else
