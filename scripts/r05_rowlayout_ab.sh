@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the handle's own row layout (PV_ROW_LAYOUT=run vs natural) for c3 / c4, after the
-# Needs scripts/r05_row_layout.patch applied (git apply) and the library rebuilt: PV_ROW_LAYOUT is not in the product.
 # GPU suite with the run-major layout.  Stops at the first failing step.
+# Needs scripts/r05_row_layout.patch applied (git apply) and the library rebuilt: PV_ROW_LAYOUT is not in the product.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
