@@ -301,13 +301,16 @@ __device__ __forceinline__ void synth_frame(const float2 (&sv)[Geo<L>::E + 1], b
         if constexpr (Q1) {
             PV_FOR_BINS(E, lane, { phc[i] = __builtin_fmaf(pm.rho_rev, ph[i], 0.0f); })
         } else if constexpr (RACC) {
-            const float npq = -pm.p_over_q;  // -(p mod q) / q
+            // -(p mod q) / q; +0 on a run's first frame (wave-uniform, one scalar select):
+            // R <- fract(fma(mr, +0, R)) = fract(R) = R bit for bit, since R is in [0, 1) and
+            // mr is finite (contract v4) — no per-bin select
+            const float npq = add_decision ? -pm.p_over_q : 0.0f;
             const float tqf = (float)tq;
             PV_FOR_BINS(E, lane, {
                 // m = -rint(dev); R <- fract(R - m p/q) = fract(R + rint(dev) p/q)
                 const float mr = unwrap_round(ph[i], phprev[i], ekv[i]);
                 float R = __int_as_float(M[i]);
-                if (add_decision) R = __builtin_amdgcn_fractf(__builtin_fmaf(mr, npq, R));
+                R = __builtin_amdgcn_fractf(__builtin_fmaf(mr, npq, R));
                 M[i] = __float_as_int(R);
                 phprev[i] = ph[i];
                 const float tj = __builtin_amdgcn_fractf(tqf * __uint_as_float(jkv[i]));
