@@ -90,12 +90,39 @@ __global__ __launch_bounds__(256) void k_fft_small(const float2* __restrict__ in
 // registers with compile-time indices (the twiddle of every butterfly is a wave-uniform
 // table entry -> scalar loads), W = 1 / exactly -i in the first two stages as in the
 // register-blocked engine; 16-byte loads and stores of the lane's contiguous transform.
+// N = 8, 16: the lane's transform is N/2 16-byte pieces N * 8 bytes apart from its
+// neighbour lanes', so every load instruction of a wave spans 64 separate pieces; the block's
+// 256 transforms (one contiguous stretch of 256 N points) are instead moved with wave-
+// contiguous 16-byte loads / stores staged through LDS (rows of N/2 + 1 pieces: the pad
+// spreads the lanes' row reads over the banks).
 template <int N, bool INV>
 __global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, float2* out,
                                                   const float2* __restrict__ tw, int batch) {
-    const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (b >= batch) return;
+    constexpr bool STAGE = (N == 8 || N == 16);  // (N = 4 staged: 5.63 -> 5.62 TB/s, not kept)
+    constexpr int H = N / 2, ROW = H + 1;  // 16-byte pieces per transform, LDS row length
+    __shared__ float4 st[STAGE ? 256 * ROW : 1];
+    const long long b0 = (long long)blockIdx.x * 256;
+    const long long b = b0 + threadIdx.x;
+    const int nv = (int)min(256LL, (long long)batch - b0);  // transforms of this block
     f2v x[N];
+    if constexpr (STAGE) {
+        const float4* src = reinterpret_cast<const float4*>(in + b0 * N);
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+            const int e = threadIdx.x + 256 * q;  // piece e of the block: transform e / H
+            if (e < nv * H) st[(e / H) * ROW + e % H] = src[e];
+        }
+        __syncthreads();
+        if (b < batch) {
+#pragma unroll
+            for (int q = 0; q < H; ++q) {
+                const float4 v = st[threadIdx.x * ROW + q];
+                x[2 * q] = f2v{v.x, v.y};
+                x[2 * q + 1] = f2v{v.z, v.w};
+            }
+        }
+    } else {
+    if (b >= batch) return;
     if constexpr (N == 2) {
         const float2 a0 = in[b * 2], a1 = in[b * 2 + 1];
         x[0] = f2v{a0.x, a0.y};
@@ -109,6 +136,7 @@ __global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, 
             x[2 * q + 1] = f2v{v.z, v.w};
         }
     }
+    }  // !STAGE
 #pragma unroll
     for (int Ns = 1; Ns < N; Ns <<= 1) {
         f2v y[N];
@@ -135,7 +163,19 @@ __global__ __launch_bounds__(256) void k_fft_reg(const float2* __restrict__ in, 
 #pragma unroll
         for (int q = 0; q < N; ++q) x[q] = y[q];
     }
-    if constexpr (N == 2) {
+    if constexpr (STAGE) {
+        // every thread's own row only: the barrier orders the block's reads above before
+        // any store below (in-place use is safe)
+#pragma unroll
+        for (int q = 0; q < H; ++q) st[threadIdx.x * ROW + q] = make_float4(x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y);
+        __syncthreads();
+        float4* dst = reinterpret_cast<float4*>(out + b0 * N);
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+            const int e = threadIdx.x + 256 * q;
+            if (e < nv * H) dst[e] = st[(e / H) * ROW + e % H];
+        }
+    } else if constexpr (N == 2) {
         out[b * 2] = make_float2(x[0].x, x[0].y);
         out[b * 2 + 1] = make_float2(x[1].x, x[1].y);
     } else {

@@ -45,7 +45,7 @@ static int check_file(const char* in, int N, const char* out, bool inverse) {
 }
 
 static int bench() {
-    const int sizes[] = {32, 64, 128, 256, 512, 1024, 2048};
+    const int sizes[] = {2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048};
     const int batch = 65536;
     float2 *sig = nullptr, *inter = nullptr, *big = nullptr;
     (void)hipMalloc((void**)&sig, sizeof(float2) * 2048);
@@ -68,7 +68,8 @@ static int bench() {
             FFT::HPFFT::timer().endGpuTimer();
             acc += FFT::HPFFT::timer().getGpuElapsedTimeForPreviousOperation();
         }
-        const int nb = (int)((size_t)batch * 2048 / N > (size_t)1 << 24 ? (1 << 24) / N : (size_t)batch * 2048 / N);
+        // the whole 1 GiB buffer at every N (2^27 points): no size fits the 256 MB MALL
+        const int nb = (int)((size_t)batch * 2048 / N);
         for (int i = 0; i < 3; ++i) (void)pv_fft_c2c((pv_float2*)big, (pv_float2*)big, N, nb, 0, nullptr);
         (void)hipEventRecord(e0);
         const int breps = 20;

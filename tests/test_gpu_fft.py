@@ -73,6 +73,28 @@ def test_fft_small_n_offset_buffers_and_ragged_batch(cuda, n):
         assert complex(outb[0].item()) == 7.0 + 0j and complex(outb[-1].item()) == 7.0 + 0j
 
 
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_fft_register_path_partial_blocks(cuda, n):
+    """n <= 16 on 16-byte aligned buffers (k_fft_reg; n = 4 .. 16 stage the block's 256
+    transforms through LDS): batches that end inside a 256-transform block, out of place and
+    in place, every transform against the oracle, nothing written past the batch."""
+    import torch
+    from pvamd.fft import fft
+    rng = np.random.default_rng(200 + n)
+    for B in (1, 255, 257, 300):
+        x = (rng.standard_normal((B, n)) + 1j * rng.standard_normal((B, n))).astype(np.complex64)
+        r = np.stack([pvref.fft_c64(x[b]) for b in range(B)])
+        src = torch.from_numpy(x).cuda()
+        outb = torch.full((B + 1, n), 7.0 + 0j, dtype=torch.complex64, device="cuda")
+        fft(src, out=outb[:B])
+        g = outb.cpu().numpy()
+        for b in range(B):
+            assert rel_err(g[b], r[b]) <= tol(n), (n, B, b)
+        assert np.all(g[B] == 7.0 + 0j)
+        fft(src, out=src)  # in place
+        assert np.array_equal(src.cpu().numpy(), g[:B])
+
+
 @pytest.mark.parametrize("name", ["50Hz", "50Hz+500Hz", "500Hz+505Hz+12000Hz"])
 def test_fft_reference_dat_fixtures(cuda, name):
     """The reference's FFT benchmark inputs (src/<tone>/*.dat), first 512 samples."""
