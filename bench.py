@@ -246,7 +246,9 @@ def main():
     cdev = dev if backend == "nccl" else torch.device("cpu")
 
     from pvamd import PITCH_SHIFT, REF_COMPAT, PhaseVocoder, STANDARD, TIME_SHIFT
-    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED, diagnostic_build
+    from pvamd._lib import PV_SPEC_NATURAL, PV_SPEC_PACKED, diagnostic_build, lib as _pvlib
+    # the loaded library's source hash (pvamd._lib refuses one that is not this tree's)
+    lib_sha = _pvlib().pv_sources_sha().decode()
     # a diagnostic build (timing-only ablations: wrong outputs) is for --no-check A/B runs only
     diag = diagnostic_build()
     if diag and not args.no_check:
@@ -418,7 +420,11 @@ def main():
             check["pass"] = bool(t[2] == 0)
             check["all_finite"] = bool(t[3] == 0)
     B_read = N // 2 + 1 if compat else B
-    path_bytes = (4 * hop_a + 4 * hop_s + 8 * B + 8 * B_read) * C * frames * world * args.steps
+    # HBM bytes of the whole path per frame: input and output samples, plus the spectrum row
+    # written and re-read when it goes through HBM (the split path); a single launch that keeps
+    # the spectrum on chip moves only the samples (SURVEY §8(d) fused-mode bytes)
+    path_bytes_per_frame = 4 * hop_a + 4 * hop_s + (0 if spec_on_chip else 8 * B + 8 * B_read)
+    path_bytes = path_bytes_per_frame * C * frames * world * args.steps
 
     cpu = None
     # the CPU baseline is a rank-0, N = 1 figure (the contract's cpu_baseline): an N-rank run
@@ -447,7 +453,9 @@ def main():
                        "dist_backend": backend if distributed else None},
             "roofline": roof,
             "diagnostic_build": diag,
+            "lib_sources_sha": lib_sha,
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
+            "path_bytes_per_frame": path_bytes_per_frame,
             "measured_ceiling": ceiling,
             "kernels": kernels,
             "kernel_timing": "block: one event pair around the timed loop" if block
@@ -503,14 +511,10 @@ def alg_flops_per_frame(kernel, N, compat):
 
 
 def kernel_sources_sha():
-    """sha256[:16] of the kernel sources, as scripts/isa_static.py records it"""
-    import hashlib
-    d = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
-    h = hashlib.sha256()
-    for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".hpp", ".h")):
-            h.update(open(os.path.join(d, f), "rb").read())
-    return h.hexdigest()[:16]
+    """sha256[:16] of the library's sources (pvamd._lib.sources_sha, the hash the Makefile
+    compiles into libpv.so and scripts/isa_static.py records)"""
+    from pvamd._lib import sources_sha
+    return sources_sha()
 
 
 # a roof "binds" when the kernel reaches this fraction of it; below it on both roofs the

@@ -175,6 +175,10 @@ int pv_contract_version(void);
 /* 1 for a diagnostic build (timing-only ablations or instrumentation compiled in with
  * PV_DIAGNOSTIC_BUILD: outputs are not the product's), 0 for the product */
 int pv_diagnostic_build(void);
+/* sha256[:16] of the sources this library was built from (phase-vocoder_amd/csrc: every
+ * *.hip *.hpp *.h *.cpp and the Makefile in byte order, then include/pv.h), compiled in by the
+ * Makefile: the Python binding refuses a library whose hash is not its tree's */
+const char* pv_sources_sha(void);
 const char* pv_status_string(pv_status s);
 const char* pv_last_error(void); /* thread-local text of the last failure */
 

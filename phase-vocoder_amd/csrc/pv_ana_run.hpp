@@ -62,8 +62,8 @@ constexpr int row_stores() { return PACKED ? E : E + 1; }
 // another launch, long after they would have left the caches).  rec (nullable): the run
 // record {S, phi(t0), phi(t0 + nfr - 1)} (kRecFields rows of bins_pad words, phases as their
 // float bits).
-template <int L, bool EKL, int D, bool PACKED, int RING = 0, int NA = Geo<L>::E>
-__device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile, float* ring,
+template <int L, bool EKL, int D, bool PACKED, int NA = Geo<L>::E>
+__device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, float2* tile,
                                         const float2 (&tw0)[Geo<L>::E], int lane, int c, int t0, int nfr,
                                         float e_lane, int* rec, float (&phprev)[Geo<L>::E + 1],
                                         ana_acc_t<L> (&sacc)[Geo<L>::E + 1]) {
@@ -97,6 +97,25 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     float2* specc = p.spec + (long long)c * p.ld_spec;
     using Acc = ana_acc_t<L>;
     PV_FOR_BINS(E, lane, { phprev[i] = 0.0f; sacc[i] = Acc(0); })
+    // mirrored-pair split (frame below): every bin analysed, L <= 512 (the L = 1024 kernels
+    // sit at their VGPR bound)
+#ifdef PV_ANA_NOPAIR
+    constexpr bool PAIR = false;
+#else
+    constexpr bool PAIR = (NA == E) && (L <= 512);
+#endif
+    constexpr int H = E / 2;
+    const int rev = ((64 - lane) & 63) << 2;            // lane reversal l -> (64 - l) mod 64
+    const float2* baseT = twsl + lane;                  // split twiddles of the lane's bins
+    const int offP = L - lane;                          // partner bins L - lane - 64 i
+    const int offP0 = (lane == 0) ? L / 2 : L - lane;   // pair 0's partner (lane 0: bin L/2)
+    const float2* baseP = twsl + offP;
+    const float2* baseP0 = twsl + offP0;
+    const float* eklP = ekl + offP;
+    const float* eklP0 = ekl + offP0;
+    // e_k of the partner bins: k mod 64 = (64 - lane) mod 64
+    const float e_lane_p = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(e_lane)));
+    (void)H; (void)baseT; (void)baseP; (void)baseP0; (void)eklP; (void)eklP0; (void)e_lane_p;
 
     // One frame: window + FFT + split + atan2, spectrum row, decisions, from raw samples.
     auto window = [&](const float2 (&xr)[E], float2 (&z)[E]) {
@@ -119,8 +138,10 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     // made the compiler copy in-flight prefetch registers: scripts/prefetch_hazards.py)
     static_assert(NA % CH == 0 && NA >= CH && NA <= E, "whole chunks");
     auto frame = [&](int u, float2 (&z)[E]) {
-        float2* srow = specc + (long long)(t0 + u) * p.spec_stride + lane;
-        (void)srow;
+        float2* prow = specc + (long long)(t0 + u) * p.spec_stride;  // the row
+        float2* srow = prow + lane;
+        float2* rrow = prow + ((64 - lane) & 63);  // lane-reversed block positions
+        (void)srow; (void)prow; (void)rrow;
         // the last pass's registers feed the split directly (no final image in LDS)
 #ifndef PV_ABL_NOFFT
         fft_run<L, false, false, 0, ana_tws_min<L>()>(z, tile, twl, tw0, lane, twsl);
@@ -144,6 +165,104 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         }
         phprev[E] = phL;
         }
+        if constexpr (PAIR) {
+            // Mirrored pairs: pair i of lane l is bin k = l + 64 i (i < E/2, slot i) and bin
+            // L - k (slot E-1-i), whose split operands are the same A = Z[k], B = Z[L - k]
+            // swapped: er, or are the same sums, ei, oi the negated differences (exact), so
+            // both bins come from one permute and one set of terms — bit for bit the
+            // per-bin formula (contract v2).  Lane 0's partners are bins 64 (E - i), and its
+            // pair 0 is (bin 0, bin L/2), bin L/2 being the one bin that is its own mirror:
+            // its operands (Z[L/2] twice) come in by a lane-0 select.
+            // Row stores: pair i's own bins fill block i; its partners fill block E-1-i at
+            // positions 64 (E-1-i) + (64 - l) (l >= 1), whose position 0 is lane 0's partner of
+            // pair i + 1 (of pair 0 for the last block, bin L/2).  So each partner store waits
+            // for the next pair and takes lane 0's value from it: every store is one aligned
+            // 512-byte block (a straddling store measured 15 % slower).
+            f2v pprev;         // the previous pair's partner {mag, phase}
+            unsigned h0m = 0, h0p = 0;  // lane 0's pair-0 partner (bin L/2), as SGPR bits
+            static_for<0, H>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const float2 A = z[slot_reg<L>(i)];
+                const float2 o = z[slot_reg<L>(E - 1 - i)];
+                const float2 m = z[slot_reg<L>((E - i) & (E - 1))];
+                float2 Bz;
+                Bz.x = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(o.x)));
+                Bz.y = __int_as_float(__builtin_amdgcn_ds_bpermute(rev, __float_as_int(o.y)));
+                lane0_mov2(Bz.x, Bz.y, m.x, m.y);  // lane 0 read itself: its partner is m
+                const float2 tw = lds_ld(&baseT[64 * i]);
+                const float2 twp = lds_ld(i == 0 ? baseP0 : &baseP[-64 * i]);
+                const float er = A.x + Bz.x, ei = A.y - Bz.y, orr = A.y + Bz.y, oi = Bz.x - A.x;
+                float Xr = __builtin_fmaf(orr, tw.x, __builtin_fmaf(-oi, tw.y, er));  // contract v2
+                float Xi = __builtin_fmaf(orr, tw.y, __builtin_fmaf(oi, tw.x, ei));
+                float Xrp, Xip;
+                if constexpr (i == 0) {
+                    if (lane == 0) Xi = 0.0f;  // bin 0 is real
+                    // the partner's own operands (B, A), on lane 0 (Z[L/2], Z[L/2])
+                    const float2 h = z[slot_reg<L>(H)];
+                    const bool l0 = lane == 0;
+                    const float ax = l0 ? h.x : Bz.x, ay = l0 ? h.y : Bz.y;
+                    const float bx = l0 ? h.x : A.x, by = l0 ? h.y : A.y;
+                    const float erp = ax + bx, eip = ay - by, orp = ay + by, oip = bx - ax;
+                    Xrp = __builtin_fmaf(orp, twp.x, __builtin_fmaf(-oip, twp.y, erp));
+                    Xip = __builtin_fmaf(orp, twp.y, __builtin_fmaf(oip, twp.x, eip));
+                } else {
+                    // partner terms (er, -ei, or, -oi)
+                    Xrp = __builtin_fmaf(orr, twp.x, __builtin_fmaf(oi, twp.y, er));
+                    Xip = __builtin_fmaf(orr, twp.y, __builtin_fmaf(-oi, twp.x, -ei));
+                }
+#ifdef PV_ABL_NOATAN
+                const f2v ph2 = f2v{Xi, Xip};
+#else
+                const f2v ph2 = atan2_pv2(Xi, Xr, Xip, Xrp);
+#endif
+                const float mag = half_sqrt(__builtin_fmaf(Xr, Xr, Xi * Xi));
+                const float magp = half_sqrt(__builtin_fmaf(Xrp, Xrp, Xip * Xip));
+                constexpr int sp = E - 1 - i;  // the partner's slot
+                const Acc mb = decision_term<Acc>(ph2.x, phprev[i], EKL ? lds_ld(&ekl[lane + 64 * i]) : e_lane);
+                const Acc mp = decision_term<Acc>(ph2.y, phprev[sp], EKL ? lds_ld(i == 0 ? &eklP0[0] : &eklP[-64 * i]) : e_lane_p);
+                sacc[i] += mb;
+                sacc[sp] += mp;
+                if (u == 0) {
+                    sacc[i] -= mb;
+                    sacc[sp] -= mp;
+                    if (rec != nullptr) {
+                        rec[BP + lane + 64 * i] = __float_as_int(ph2.x);
+                        rec[BP + (i == 0 ? offP0 : offP - 64 * i)] = __float_as_int(ph2.y);
+                    }
+                }
+                phprev[i] = ph2.x;
+                phprev[sp] = ph2.y;
+#ifdef PV_ABL_NOSTORE
+                sink += mag + magp;
+#else
+                if constexpr (PACKED && i == 0) {
+                    const f2v s0 = (lane == 0) ? f2v{pack_real_bin(mag, ph2.x), pack_real_bin(magL, phL)}
+                                               : f2v{mag, ph2.x};
+                    __builtin_nontemporal_store(s0, reinterpret_cast<f2v*>(&srow[0]));
+                } else {
+                    __builtin_nontemporal_store(f2v{mag, ph2.x}, reinterpret_cast<f2v*>(&srow[64 * i]));
+                }
+                if constexpr (!PACKED && i == 0)
+                    __builtin_nontemporal_store(f2v{magL, phL}, reinterpret_cast<f2v*>(&srow[L - lane]));
+                if constexpr (i == 0) {
+                    h0m = __builtin_amdgcn_readfirstlane(__float_as_uint(magp));
+                    h0p = __builtin_amdgcn_readfirstlane(__float_as_uint(ph2.y));
+                } else {
+                    // block E - i: the previous pair's partners, lane 0's from this pair
+                    float sx = pprev.x, sy = pprev.y;
+                    lane0_mov2(sx, sy, magp, ph2.y);
+                    __builtin_nontemporal_store(f2v{sx, sy}, reinterpret_cast<f2v*>(&rrow[64 * (E - i)]));
+                }
+                pprev = f2v{magp, ph2.y};
+                if constexpr (i == H - 1) {
+                    // block H: the last pair's partners, lane 0's bin L/2
+                    float sx = pprev.x, sy = pprev.y;
+                    lane0_mov2(sx, sy, __uint_as_float(h0m), __uint_as_float(h0p));
+                    __builtin_nontemporal_store(f2v{sx, sy}, reinterpret_cast<f2v*>(&rrow[64 * H]));
+                }
+#endif
+            });
+        } else
         // bins 0 .. E-1 of the lane in chunks of CH (bounded live registers), all reads of a
         // chunk batched, phases of each pair through the packed atan2
         static_for<0, E / CH>([&](auto ic) {
@@ -174,7 +293,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                     // hardware v_sqrt_f32 (<= 1 ulp): magnitudes only scale the output;
                     // the phase, which drives the unwrap decisions, stays bit-exact.  X
                     // came out doubled (split_chunk_bp TWICE): halve the magnitude.
-                    const float mag = 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
+                    const float mag = half_sqrt(__builtin_fmaf(X[c2].x, X[c2].x, X[c2].y * X[c2].y));
 #ifdef PV_ABL_NOSTORE
                     sink += mag;
                     if constexpr (false) {
@@ -233,59 +352,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
     // [vmcnt(NST): x(u+1) landed, the row stores may still be in flight] [window x(u+1)].
     // The prefetch index is clamped (the last trip reloads its own frame), so the loads
     // and stores are unconditional and the count is exact (gload_pairs / vm_wait).
-    if constexpr (D > 0 && RING > 0) {
-        // LDS-DMA input ring (RING slots of hop samples per wave): frame v's hop new samples
-        // are one or two global_load_lds_dwordx4 (NDMA = hop / 256) into slot v mod RING,
-        // issued RING frames ahead of their use, so no VGPR holds samples in flight.
-        // Trip u: [frame u: NST row stores] [vmcnt: x(u+1) landed] [ds_read the lane's D
-        // pairs of x(u+1)] [window] [DMA x(u+1+RING) into the slot just read].  Ops issued
-        // after x(u+1): (RING-1) (NST + NDMA) + NST in the steady state, (RING-1) NDMA +
-        // (u+1) NST in the first trips (x(1..RING) issued before the loop) — the wait below
-        // uses that lower bound (extra record stores at u = 0 only make it conservative).
-        static_assert(D < E, "shifted input: hop < N / 2");
-        static_assert(D == 2 || D == 4, "the ring moves 1 KiB DMA pieces: hop = 256 or 512");
-        constexpr int NDMA = D / 2;
-        constexpr int HOPF = 128 * D;  // floats per slot
-        if (ufast > 0) {
-            float2 xr[E], z[E];
-            const unsigned rbase = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-            auto dma = [&](int v, int slot) {
-                const float* g = xc + (long long)(t0 + min(v, ufast - 1)) * p.hop + (N - HOPF) + 4 * lane;
-#pragma unroll
-                for (int j = 0; j < NDMA; ++j) glds16(g + 256 * j, rbase + (unsigned)(slot * HOPF + 256 * j) * 4u);
-            };
-            {
-                f2v x0[E];
-                gload_pairs<E>(x0, xc + (long long)t0 * p.hop + 2 * lane);
-#pragma unroll
-                for (int v = 1; v <= RING; ++v) dma(v, v % RING);
-                vm_wait<RING * NDMA>(x0);
-#pragma unroll
-                for (int q = 0; q < E; ++q) xr[q] = make_float2(x0[q].x, x0[q].y);
-                window(xr, z);
-            }
-            int slot = 1 % RING;  // slot of x(u + 1)
-            for (int u = 0; u < ufast; ++u) {
-                frame(u, z);  // exactly NST row stores (+ records at u = 0)
-                {
-                    const int m = min(u, RING - 1);
-                    static_for<0, RING>([&](auto mc) {
-                        constexpr int M = decltype(mc)::value;
-                        constexpr int K = (RING - 1) * NDMA + (M + 1) * NSTW;
-                        if (m == M) vm_wait_n<(K < 63 ? K : 63)>();
-                    });
-                }
-                const float* rs = ring + slot * HOPF + 2 * lane;
-#pragma unroll
-                for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
-#pragma unroll
-                for (int j = 0; j < D; ++j) xr[E - D + j] = lds_ld(reinterpret_cast<const float2*>(rs + 128 * j));
-                window(xr, z);
-                dma(u + 1 + RING, slot);
-                slot = (slot + 1 == RING) ? 0 : slot + 1;
-            }
-        }
-    } else if constexpr (D > 0) {
+    if constexpr (D > 0) {
         static_assert(D < E, "shifted input: hop < N / 2");
         if (ufast > 0) {
             float2 xr[E], z[E];
@@ -297,6 +364,47 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
 #else
             auto src = [&](int u) { return xc + (long long)(t0 + min(u, ufast - 1)) * p.hop + 2 * lane; };
 #endif
+            int u = 0;
+#ifndef PV_ANA_NOROT
+            // Register rotation: frames are walked in groups of RR = E / D, after which the
+            // window has moved by E registers.  Frame u + r (r < RR) holds its pair q in
+            // register (q + D r) mod E, so its D new pairs land in the registers frame u + r - 1
+            // no longer needs and no register is shifted (the shifting form costs 2 (E - D)
+            // v_mov per frame); the groups end at rotation 0, where the loop below continues.
+            // (L <= 512 with groups of at most 4 frames: longer unrolled groups blow up the
+            // compile, and the L = 1024 kernels sit at their VGPR bound)
+            if constexpr (E % D == 0 && E / D <= 4 && L <= 512) {
+                constexpr int RR = E / D;
+                const int umain = ufast - ufast % RR;
+                auto window_rot = [&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    const float2* wl = reinterpret_cast<const float2*>(winl) + lane;
+#pragma unroll
+                    for (int q = 0; q < E; ++q) {
+#ifdef PV_ABL_NOWIN
+                        const float2 wv = make_float2(1.0f, 1.0f);
+#else
+                        const float2 wv = lds_ld(&wl[64 * q]);
+#endif
+                        const float2 s = xr[(q + D * r) % E];
+                        z[q].x = s.x * wv.x;
+                        z[q].y = s.y * wv.y;
+                    }
+                };
+                for (; u < umain; u += RR) {
+                    static_for<0, RR>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value;
+                        f2v xv[D];  // frame u + r + 1's new pairs (logical E - D .. E - 1)
+                        gload_tail<D, E>(xv, src(u + r + 1));
+                        frame(u + r, z);  // exactly NST row stores (+ records at u = 0)
+                        vm_wait<NSTW>(xv);
+#pragma unroll
+                        for (int j = 0; j < D; ++j) xr[(D * r + j) % E] = make_float2(xv[j].x, xv[j].y);
+                        window_rot(IC<(r + 1) % RR>{});
+                    });
+                }
+            }
+#endif
             auto consume = [&](const f2v (&xv)[D]) {
 #pragma unroll
                 for (int q = 0; q < E - D; ++q) xr[q] = xr[q + D];
@@ -304,7 +412,7 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
                 for (int j = 0; j < D; ++j) xr[E - D + j] = make_float2(xv[j].x, xv[j].y);
                 window(xr, z);
             };
-            for (int u = 0; u < ufast; ++u) {
+            for (; u < ufast; ++u) {
                 f2v xv[D];  // the D new pairs of frame u+1: registers E-D .. E-1
                 gload_tail<D, E>(xv, src(u + 1));
                 frame(u, z);  // exactly NST row stores (+ records at u = 0)
@@ -345,8 +453,18 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
         window(xr, z);
         frame(u, z);
     }
-    if (rec != nullptr)
-        PV_FOR_BINS(E, lane, { rec[k] = decision_sum(sacc[i], nfr - 1); rec[2 * BP + k] = __float_as_int(phprev[i]); })
+    if (rec != nullptr) {
+        if constexpr (PAIR) {
+            // slot i < H: bin lane + 64 i; slot E-1-i: its partner; slot E (lane 0): bin L
+            PV_FOR_BINS(E, lane, {
+                const int kb = (i < H) ? k : (i == E) ? L : (i == E - 1) ? offP0 : offP - 64 * (E - 1 - i);
+                rec[kb] = decision_sum(sacc[i], nfr - 1);
+                rec[2 * BP + kb] = __float_as_int(phprev[i]);
+            })
+        } else {
+            PV_FOR_BINS(E, lane, { rec[k] = decision_sum(sacc[i], nfr - 1); rec[2 * BP + k] = __float_as_int(phprev[i]); })
+        }
+    }
 #ifdef PV_ABL_NOSTORE
     if (sink == 1234.5f && rec != nullptr) rec[lane] = 0;  // keeps the magnitudes computed
 #endif

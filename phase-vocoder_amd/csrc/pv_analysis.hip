@@ -15,45 +15,31 @@ namespace pv {
 // EKL: the expected advance e_k from an LDS table; otherwise (64 a multiple of the hop
 // divisor, so e_k depends on k mod 64 only) one register per lane, e_k = ek[lane].
 // waves per SIMD the analysis is compiled for (__launch_bounds__): L = 512 at <= 128 VGPRs
-// (94 used), L = 1024 at <= 168 (LDS with the twiddle sharing allows 3 workgroups per CU)
+// (112 used with the 4-frame register rotation of ana_run; at 5 waves it spills), L = 1024
+// at <= 168 (LDS with the twiddle sharing allows 3 workgroups per CU)
 constexpr int kAnaWaves512 = 4;
 constexpr int kAnaWaves1024 = 3;
 // D > 0: hop = 128 D samples, so frame u+1's register q is frame u's register q + D and a
 // frame costs only its D new sample pairs per lane (the other E - D are shifted in
 // registers): 1/E of the frame's bytes leave L2 instead of all of them.
 // PACKED: the pv.h PV_SPEC_PACKED row layout (bin L folded into slot 0).
-// Input ring (PV_ANA_RING = R > 0, hop = 256 or 512): each wave streams its frames' new
-// samples R frames ahead into R LDS slots by LDS-DMA (ana_run); the workgroup is then W =
-// PV_ANA_WAVES waves sharing one copy of the tables (the ring's LDS is paid by the tables'
-// duplication across 4-wave workgroups instead of by occupancy).
-#ifndef PV_ANA_RING
-#define PV_ANA_RING 0
-#endif
-#ifndef PV_ANA_WAVES
-#define PV_ANA_WAVES 10
-#endif
-#ifndef PV_ANA_BIGWG
-#define PV_ANA_BIGWG 0
-#endif
-template <int L, int D>
-constexpr int ana_ring() { return (D == 2 && L == 512) ? PV_ANA_RING : 0; }
-template <int L, int D>
-constexpr int ana_waves() { return (ana_ring<L, D>() > 0 || (PV_ANA_BIGWG && D == 2 && L == 512)) ? PV_ANA_WAVES : 4; }
+// (Round 5 measured an LDS-DMA input ring R frames ahead in larger workgroups: no gain,
+// profiles/r05_ab_ring.json; the code is kept out of the product as scripts/r05_ana_ring.patch.)
+constexpr int kAnaWG = 4;  // waves (runs) per workgroup
 
 // NA: lane registers analysed (Geo<L>::E = all; fewer: bins >= 64 NA not analysed, zeros in
 // their row slots — pv_process without a spectrum output, ana_run)
-template <int L, bool EKL, int D, bool PACKED, int W = ana_waves<L, D>(), int RING = ana_ring<L, D>(),
-          int NA = Geo<L>::E>
-__global__ __launch_bounds__(64 * W, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
+template <int L, bool EKL, int D, bool PACKED, int NA = Geo<L>::E>
+__global__ __launch_bounds__(64 * kAnaWG, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;
     constexpr int E = G_::E;
     constexpr int N = 2 * L;
     constexpr int B = L + 1;
+    constexpr int W = kAnaWG;
     constexpr int NT = 64 * W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int TWN = ana_twl_n<L>();
-    float* rings = reinterpret_cast<float*>(smem);    // W x RING x hop samples (LDS-DMA ring)
-    float2* twl = reinterpret_cast<float2*>(rings + W * RING * 128 * D);  // TWN stage-major twiddles (L, or L/4)
+    float2* twl = reinterpret_cast<float2*>(smem);    // TWN stage-major twiddles (L, or L/4)
     float2* twsl = twl + TWN;                         // L+1 split twiddles (+1 pad)
     float2* tiles = twsl + (L + 2);                   // W x TILE
     float* winl = reinterpret_cast<float*>(tiles + W * G_::TILE);  // N
@@ -80,8 +66,8 @@ __global__ __launch_bounds__(64 * W, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 :
     int* rec = (p.runsum != nullptr) ? p.runsum + ((long long)c * p.nruns + run) * kRecFields * p.bins_pad : nullptr;
     float phprev[E + 1];
     ana_acc_t<L> sacc[E + 1];
-    ana_run<L, EKL, D, PACKED, RING, NA>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, rings + w * RING * 128 * D,
-                                     tw0, lane, c, t0, nfr, e_lane, rec, phprev, sacc);
+    ana_run<L, EKL, D, PACKED, NA>(p, AnaLds{twl, twsl, winl, ekl}, tiles + w * G_::TILE, tw0, lane, c, t0, nfr, e_lane,
+                                   rec, phprev, sacc);
 }
 
 // ------------------------------------------------------------------ K1 REF_COMPAT
@@ -240,11 +226,9 @@ __global__ __launch_bounds__(256) void k_compat_analysis(AnaParams p) {
 
 
 // ------------------------------------------------------------------ launchers
-template <int L, int D = 0>
+template <int L>
 static size_t ana_lds_std(bool ekl) {
-    constexpr int W = ana_waves<L, D>(), R = ana_ring<L, D>();
-    return sizeof(float) * W * R * 128 * D + sizeof(float2) * (ana_twl_n<L>() + (L + 2) + W * Geo<L>::TILE) +
-           sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
+    return sizeof(float2) * (ana_twl_n<L>() + (L + 2) + kAnaWG * Geo<L>::TILE) + sizeof(float) * (2 * L + (ekl ? L + 1 : 0));
 }
 template <int L>
 static size_t ana_lds_compat() {
@@ -271,24 +255,20 @@ static hipError_t launch_std_analysis_t(int L, dim3 grid, const AnaParams& p, hi
         if (p.ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
             constexpr int E_ = LL / 64;  // D < E (instantiated for every L, run for the checked ones)
             constexpr int D1 = (1 < E_) ? 1 : 0, D2 = (2 < E_) ? 2 : 0, D4 = (4 < E_) ? 4 : 0;
-            auto go = [&](auto kern, int W, size_t lds) {
-                const dim3 g((p.nruns + W - 1) / W, grid.y);
-                hipLaunchKernelGGL(kern, g, dim3(64 * W), lds, s, p);
-            };
-            if (d == 1) go(k_std_analysis<LL, false, D1, PK>, ana_waves<LL, D1>(), ana_lds_std<LL, D1>(false));
-            else if (d == 2) go(k_std_analysis<LL, false, D2, PK>, ana_waves<LL, D2>(), ana_lds_std<LL, D2>(false));
+            const size_t lds = ana_lds_std<LL>(false);
+            auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(64 * kAnaWG), lds, s, p); };
+            if (d == 1) go(k_std_analysis<LL, false, D1, PK>);
+            else if (d == 2) go(k_std_analysis<LL, false, D2, PK>);
             else if (LL == 1024 && PK && p.src_hi < LL) {
                 // bins above src_hi unread (config 4, pitch 1.5: 684 .. 1024): the registers
                 // analysed, in whole chunks of kAnaChunk
-                constexpr int W4 = ana_waves<LL, D4>(), R4 = ana_ring<LL, D4>();
                 const int na = kAnaChunk * ((p.src_hi + 64 * kAnaChunk) / (64 * kAnaChunk));
-                const size_t lds = ana_lds_std<LL, D4>(false);
-                if (na <= 8) go(k_std_analysis<LL, false, D4, PK, W4, R4, (8 < E_ ? 8 : E_)>, W4, lds);
-                else if (na <= 10) go(k_std_analysis<LL, false, D4, PK, W4, R4, (10 < E_ ? 10 : E_)>, W4, lds);
-                else if (na <= 12) go(k_std_analysis<LL, false, D4, PK, W4, R4, (12 < E_ ? 12 : E_)>, W4, lds);
-                else if (na <= 14) go(k_std_analysis<LL, false, D4, PK, W4, R4, (14 < E_ ? 14 : E_)>, W4, lds);
-                else go(k_std_analysis<LL, false, D4, PK>, W4, lds);
-            } else go(k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
+                if (na <= 8) go(k_std_analysis<LL, false, D4, PK, (8 < E_ ? 8 : E_)>);
+                else if (na <= 10) go(k_std_analysis<LL, false, D4, PK, (10 < E_ ? 10 : E_)>);
+                else if (na <= 12) go(k_std_analysis<LL, false, D4, PK, (12 < E_ ? 12 : E_)>);
+                else if (na <= 14) go(k_std_analysis<LL, false, D4, PK, (14 < E_ ? 14 : E_)>);
+                else go(k_std_analysis<LL, false, D4, PK>);
+            } else go(k_std_analysis<LL, false, D4, PK>);
         } else if (p.ek_lane) hipLaunchKernelGGL((k_std_analysis<LL, false, 0, PK>), grid, dim3(256), ana_lds_std<LL>(false), s, p);
         else hipLaunchKernelGGL((k_std_analysis<LL, true, 0, PK>), grid, dim3(256), ana_lds_std<LL>(true), s, p);
     });
@@ -312,9 +292,9 @@ static int std_analysis_wgs_per_cu_t(int L, int hop, bool ek_lane, int* waves_pe
         if (ek_lane && LL >= 256 && LL <= 1024 && (d == 1 || d == 2 || d == 4) && d < LL / 64) {
             constexpr int E_ = LL / 64;
             constexpr int D1 = (1 < E_) ? 1 : 0, D2 = (2 < E_) ? 2 : 0, D4 = (4 < E_) ? 4 : 0;
-            if (d == 1) occ((const void*)k_std_analysis<LL, false, D1, PK>, ana_waves<LL, D1>(), ana_lds_std<LL, D1>(false));
-            else if (d == 2) occ((const void*)k_std_analysis<LL, false, D2, PK>, ana_waves<LL, D2>(), ana_lds_std<LL, D2>(false));
-            else occ((const void*)k_std_analysis<LL, false, D4, PK>, ana_waves<LL, D4>(), ana_lds_std<LL, D4>(false));
+            if (d == 1) occ((const void*)k_std_analysis<LL, false, D1, PK>, kAnaWG, ana_lds_std<LL>(false));
+            else if (d == 2) occ((const void*)k_std_analysis<LL, false, D2, PK>, kAnaWG, ana_lds_std<LL>(false));
+            else occ((const void*)k_std_analysis<LL, false, D4, PK>, kAnaWG, ana_lds_std<LL>(false));
         } else if (ek_lane) occ((const void*)k_std_analysis<LL, false, 0, PK>, 4, ana_lds_std<LL>(false));
         else occ((const void*)k_std_analysis<LL, true, 0, PK>, 4, ana_lds_std<LL>(true));
     });

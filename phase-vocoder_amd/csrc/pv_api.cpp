@@ -503,6 +503,10 @@ int pv_abi_version(void) { return PV_ABI_VERSION; }
 // 2 (round 4): fused real-split accumulation, one-rounding unwrap decision (pv_device.hpp);
 // 3: twiddle-first radix-E FFT passes with the window folded in, L <= 512 (fft_pass v3)
 int pv_contract_version(void) { return 4; }
+#ifndef PV_SOURCES_SHA
+#define PV_SOURCES_SHA "unset"
+#endif
+const char* pv_sources_sha(void) { return PV_SOURCES_SHA; }
 int pv_diagnostic_build(void) {
 #ifdef PV_DIAGNOSTIC_BUILD
     return 1;
@@ -668,7 +672,7 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     // Large STANDARD batches at L <= 512: the analysis grid runs in rounds of (workgroups one
     // CU holds) x CUs, and a last partial round leaves most of the chip idle while its runs
     // finish.  Among F = 48, 56, .. 96 take the one with the fewest frame-times, rounds x F
-    // (ties: the shorter runs).  Config 3 (1024 x 1722 frames, 5 workgroups per CU): 48 gives
+    // (near-ties: the longer runs, below).  Config 3 at round 5's 5 workgroups per CU: 48 gives
     // 9216 workgroups = 8 rounds (the last a fifth full) x 48 = 384, 88 gives 5120 = 4 x 88 =
     // 352 (measured on two boxes: +1.7 / +1.8 % frames/s, profiles/r04_ab_c3_F.txt; what the
     // longer runs buy is the carry, seam and synthesis time — the analysis kernel itself is
@@ -686,12 +690,18 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
         if (wpc > 0) {
             const long long slots = (long long)kRoundCUs * wpc;
             const long long C = std::max(cfg->max_channels, 1), T = std::max(cfg->max_frames, 1);
+            // (round 6: the longest run within 2 % of the fewest frame-times — each run costs a
+            // record, a carry and a seam; with the 4-wave/SIMD analysis config 3 has 48 -> 432
+            // and 88 -> 440 frame-times, and F = 88 measured +1.9 % frames/s over 48)
             long long best = -1;
-            for (int f = 48; f <= 96; f += 8) {
+            long long cost_of[7];
+            for (int j = 0, f = 48; f <= 96; f += 8, ++j) {
                 const long long wgs = C * (((T + f - 1) / f + W - 1) / W);
-                const long long cost = ((wgs + slots - 1) / slots) * f;
-                if (best < 0 || cost < best) { best = cost; F = f; }
+                cost_of[j] = ((wgs + slots - 1) / slots) * f;
+                if (best < 0 || cost_of[j] < best) best = cost_of[j];
             }
+            for (int j = 0, f = 48; f <= 96; f += 8, ++j)
+                if (cost_of[j] * 100 <= best * 102) F = f;
         }
     }
     // tuning override (even, 8..256): PV_RUN_FRAMES

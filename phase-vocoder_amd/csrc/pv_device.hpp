@@ -174,34 +174,6 @@ __device__ __forceinline__ void vm_wait(f2v (&xr)[E]) {
     for (int q = 0; q < E; ++q) asm volatile("" : "+v"(xr[q]));  // uses stay after the wait
 }
 
-// a bare vmcnt wait (no registers to pin: the data of an LDS-DMA lands in LDS)
-template <int K>
-__device__ __forceinline__ void vm_wait_n() {
-    static_assert(K >= 0 && K <= 63, "vmcnt is 6 bits on gfx950");
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K) : "memory");
-}
-
-// LDS-DMA (gfx950 global_load_lds_dwordx4): each lane's 16 bytes at gsrc land at LDS byte
-// address lds + 16 lane (lds = M0, wave-uniform), no VGPR destination.  M0 is reserved by
-// the compiler and written in the same statement (saved and restored, `s_nop 0` for the M0
-// hazard).  Like gload_pairs it is invisible to the compiler's wait insertion: the caller
-// counts it in vmcnt (vm_wait_n) before a ds_read of the bytes.  lgkmcnt(0) first: the
-// wave's earlier ds_reads of the slot it overwrites have returned.
-__device__ __forceinline__ void glds16(const float* gsrc, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %2\n\t"
-                 "s_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
-}
-// LDS byte address of a pointer into __shared__ memory
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(unsigned long)(const PV_LDS void*)p;
-}
-
 // Lane 0 only: (bx, by) <- (ax, ay) by two v_mov_b32 under exec & 1 (the lane-0 partner fix-up
 // of the real-FFT splits, whose partner bins are lane 0's own registers).  A v_mov issues at
 // the full VALU rate, a v_cndmask_b32 select at half (profiles/r04_valu_probe3.jsonl: 2.25 vs
@@ -369,6 +341,10 @@ __device__ __forceinline__ void sincos_rev(float rev, float* sn, float* cs) {
     *sn = __builtin_amdgcn_sinf(rev);
     *cs = __builtin_amdgcn_cosf(rev);
 }
+
+// |X| from |2X|^2 = fma(2X.re, 2X.re, (2X.im)^2) (the analysis' doubled split): hardware
+// v_sqrt_f32 (<= 1 ulp), halved exactly
+__device__ __forceinline__ float half_sqrt(float s2) { return 0.5f * __builtin_amdgcn_sqrtf(s2); }
 
 // unwrap decision of the contract (oracle pvr_unwrap_count, contract v2): the exact product
 // d * (1/2pi) rounded once onto the integer grid of [2^23, 2^24) by an fma with the magic

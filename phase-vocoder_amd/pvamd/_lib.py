@@ -58,6 +58,19 @@ def new_info() -> pv_info:
 
 
 _lib = None
+CSRC = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
+
+
+def sources_sha() -> str:
+    """sha256[:16] of the library's sources as the Makefile computes it (SHA_FILES: every
+    *.hip *.hpp *.h *.cpp in csrc/ and the Makefile in byte order, then include/pv.h)"""
+    import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h", ".cpp")) or f == "Makefile")
+    h = hashlib.sha256()
+    for p in [os.path.join(CSRC, f) for f in names] + [HEADER]:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def declared_symbols() -> list[str]:
@@ -76,6 +89,13 @@ def lib():
                           "(no CPU fallback exists)")
     L = ctypes.CDLL(os.path.abspath(LIB_PATH))
     vp, ll, i, f = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
+    # a library built from other sources than this tree's (a stale build shipped with the
+    # tree, or a leftover) is refused: `make` rebuilds it
+    L.pv_sources_sha.restype = ctypes.c_char_p
+    built, tree = L.pv_sources_sha().decode(), sources_sha()
+    if built != tree:
+        raise PVError(-1, f"{LIB_PATH} was built from sources {built}, the tree's are {tree}: "
+                          "rebuild with `make -C phase-vocoder_amd/csrc`")
     L.pv_abi_version.restype = i
     if hasattr(L, "pv_contract_version"):  # (A/B builds of older revisions lack it)
         L.pv_contract_version.restype = i

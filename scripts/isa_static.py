@@ -32,7 +32,7 @@ KERNELS = {
     ("c3", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi0ELi1ELb1ELb1E", 17),
     # config 4 (bench.py: no spectrum handed back, pitch 1.5): the instantiation analysing
     # lane registers 0 .. 11 (bins < 768; 12 square roots, no bin L)
-    ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1ELi4ELi0ELi12E", 12),
+    ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1ELi12E", 12),
     ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
@@ -57,10 +57,13 @@ FAST_EXTRA = "profiles/r04_valu_costs.json"  # measured overrides {opcode: cycle
 
 
 def sources_sha():
+    """the library's source hash (phase-vocoder_amd/pvamd/_lib.py sources_sha, the Makefile's
+    SRC_SHA): every *.hip *.hpp *.h *.cpp in csrc/ and the Makefile in byte order, then
+    include/pv.h"""
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h", ".cpp")) or f == "Makefile")
     h = hashlib.sha256()
-    for f in sorted(os.listdir(CSRC)):
-        if f.endswith((".hip", ".hpp", ".h")):
-            h.update(open(os.path.join(CSRC, f), "rb").read())
+    for p in [os.path.join(CSRC, f) for f in names] + [os.path.join(ROOT, "include", "pv.h")]:
+        h.update(open(p, "rb").read())
     return h.hexdigest()[:16]
 
 

@@ -25,6 +25,32 @@ def gpu_available() -> bool:
 
 
 @pytest.fixture(scope="session")
+def device_asm(tmp_path_factory):
+    """gfx950 assembly of the kernel sources (the Makefile's device flags) and the compiler's
+    kernel-resource-usage remarks, one parallel compile per source, shared by the tests that
+    read them: {source: (asm path, remarks text)}"""
+    import subprocess
+    d = tmp_path_factory.mktemp("asm")
+    csrc = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
+    flags = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+             "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S",
+             "-Rpass-analysis=kernel-resource-usage"]
+    procs = {}
+    for src in ("pv_analysis", "pv_kernels", "pv_fused", "pv_rt"):
+        extra = ["-fno-slp-vectorize"] if src == "pv_analysis" else []
+        out = str(d / f"{src}.s")
+        procs[src] = (out, subprocess.Popen(["/opt/rocm/bin/hipcc", *flags, *extra, "-I", os.path.join(ROOT, "include"),
+                                             "-o", out, os.path.join(csrc, f"{src}.hip")],
+                                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    res = {}
+    for src, (out, pr) in procs.items():
+        so, se = pr.communicate(timeout=900)
+        assert pr.returncode == 0, se[-2000:]
+        res[src] = (out, so + se)
+    return res
+
+
+@pytest.fixture(scope="session")
 def cuda():
     if not gpu_available():
         pytest.skip("no GPU")

@@ -22,6 +22,28 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert set(declared) <= exported
 
 
+def test_library_is_built_from_this_tree():
+    """libpv.so carries the hash of the sources it was built from (the Makefile's SRC_SHA);
+    it must be the tree's, the hash bench.py records, and the Makefile's own computation."""
+    L = _lib.lib()  # refuses a mismatch itself
+    built = L.pv_sources_sha().decode()
+    assert built == _lib.sources_sha()
+    import bench
+    assert bench.kernel_sources_sha() == built
+    mk = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "phase-vocoder_amd", "csrc"), "sources-sha"],
+                        capture_output=True, text=True, check=True).stdout.strip()
+    assert mk == built
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library whose compiled-in hash differs from the tree's is not loaded."""
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "sources_sha", lambda: "0000000000000000")
+    with pytest.raises(_lib.PVError, match="built from sources"):
+        _lib.lib()
+    monkeypatch.setattr(_lib, "_lib", None)
+
+
 def test_library_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
@@ -85,18 +107,15 @@ def test_product_does_not_reference_oracle():
 
 
 @pytest.mark.slow
-def test_prefetch_kernels_have_no_spills():
+def test_prefetch_kernels_have_no_spills(device_asm):
     """The self-tracked prefetch (gload_pairs / vm_wait, pv_device.hpp) is only sound when
     the registers it loads are never spilled or moved to AGPRs while in flight: the
     kernels that use it (analysis L <= 1024, register-OLA synthesis L <= 512) must compile
     without spills or AGPR use."""
     import re
-    import subprocess
-    csrc = os.path.join(_lib.ROOT, "phase-vocoder_amd", "csrc")
-    r = subprocess.run(["make", "-s", "-C", csrc, "resource-usage"], capture_output=True, text=True,
-                       timeout=900)
+    remarks = "\n".join(txt for _, txt in device_asm.values())
     rows, cur = {}, None
-    for line in (r.stdout + r.stderr).splitlines():
+    for line in remarks.splitlines():
         m = re.search(r"remark:\s+(.*?)\s*\[-Rpass", line)
         if not m:
             continue
@@ -107,7 +126,7 @@ def test_prefetch_kernels_have_no_spills():
         elif cur and ":" in body:
             k, v = body.split(":", 1)
             rows[cur][k.strip()] = v.strip()
-    assert rows, r.stderr[-2000:]
+    assert rows, remarks[-2000:]
     checked = 0
     for name, info in rows.items():
         m = re.match(r"_ZN2pv14k_std_analysisILi(\d+)E", name)
@@ -181,25 +200,14 @@ def test_product_library_is_not_diagnostic():
     assert _lib.diagnostic_build() is False
 
 
-def test_device_asm_has_no_prefetch_or_scc_hazards(tmp_path):
+def test_device_asm_has_no_prefetch_or_scc_hazards(device_asm):
     """The self-tracked prefetch loads (inline asm, invisible to the compiler's waits) must not
     have their registers read, written or copied before the vmcnt that retires them, and no
     inline asm that writes SCC may sit between an SCC writer and its reader
     (scripts/prefetch_hazards.py; both once produced wrong results and a GPU fault)."""
     import subprocess
     import sys
-    csrc = os.path.join(ROOT, "phase-vocoder_amd", "csrc")
-    flags = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-             "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S"]
-    procs, outs = [], []
-    for src in ("pv_analysis", "pv_kernels", "pv_fused", "pv_rt"):
-        out = str(tmp_path / f"{src}.s")
-        extra = ["-fno-slp-vectorize"] if src == "pv_analysis" else []
-        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *flags, *extra, "-I", os.path.join(ROOT, "include"),
-                                       "-o", out, os.path.join(csrc, f"{src}.hip")],
-                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
-        outs.append(out)
-    assert all(p.wait(timeout=600) == 0 for p in procs)
+    outs = [out for out, _ in device_asm.values()]
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "prefetch_hazards.py"), *outs],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("0 hazard(s)"), r.stdout[-3000:]
