@@ -97,29 +97,32 @@ def _oracle_batch(pvref, compat):
 
 
 def _port_batch(pvref, compat):
-    """What cpu_baseline times: STANDARD — the fp32 CPU port (oracle/pvport.c: the
-    contract's fp32 analysis, the integer phase scan, fp32 sin/cos, fp32 inverse FFT and
-    overlap-add, OpenMP over channels); REF_COMPAT — the fp64 restatement (no fp32 port)."""
-    return _oracle_batch(pvref, True) if compat else pvref.port_std_process_batch
+    """What cpu_baseline times: the fp32 CPU ports (oracle/pvport.c, OpenMP over channels).
+    STANDARD — the contract's fp32 analysis, the integer phase scan, fp32 sin/cos, fp32
+    inverse FFT and overlap-add; REF_COMPAT — kernel.cu's path in fp32 (2N-point real FFT,
+    sqrtf / atanf, the y-bug, N-point C2R, /N, swap, window, overlap-add)."""
+    if compat:
+        return lambda x, N, hd, e, s, fr, th: pvref.port_compat_process_batch(x, N, hd, fr, th)
+    return pvref.port_std_process_batch
 
 
 def cpu_baseline(x, N, hop_div, effect, scale, target_s=10.0, single=False, compat=False):
-    """The CPU port (oracle/pvport.c; REF_COMPAT: the fp64 restatement oracle/pvref.c; OpenMP
-    over channels) timed on a bounded sample of
+    """The fp32 CPU port (oracle/pvport.c, STANDARD or REF_COMPAT; OpenMP over channels)
+    timed on a bounded sample of
     the SAME host channels the GPU processes (x: [C, n] float32).  A single stream
     (single=True) has no channel parallelism and runs on one core."""
     pvref = _pvref()
     batch = _port_batch(pvref, compat)
-    what = ("oracle/pvref.c REF_COMPAT fp64 restatement" if compat
+    what = ("oracle/pvport.c REF_COMPAT fp32 CPU port" if compat
             else "oracle/pvport.c fp32 CPU port")
     threads, aff = cpu_share()
     C_all, n = x.shape
     frames = pvref.num_frames(n, N // hop_div)
     host = f"{threads} threads = this process's CPU share (affinity {aff}, machine {os.cpu_count()})"
-    # REF_COMPAT's checker is an fp64 restatement: slower than an fp32 CPU port of the
-    # reference would be, so the GPU/CPU ratio it gives is overstated (said in the line)
-    note = ("fp64 restatement of kernel.cu / main.cpp, not an fp32 port: an fp32 CPU port would "
-            "be faster, so the GPU/CPU ratio is overstated" if compat else
+    note = ("fp32 end to end: kernel.cu's path as a CPU port (Hamming window, shift + pad, the "
+            "2N-point real FFT, sqrtf / atanf(y/x) over all 2N bins, the y-bug, N-point C2R, /N, "
+            "swap halves, window, overlap-add); gcc -O3 -march=x86-64-v3, OpenMP over channels "
+            "(pinned to the fp64 restatement <= 1e-6 RMS, tests/test_oracle.py)" if compat else
             "fp32 end to end: the fp32-contract analysis (the GPU's own phases), the integer "
             "phase scan, fp32 sin/cos, fp32 inverse real FFT and overlap-add; gcc -O3 "
             "-march=x86-64-v3, OpenMP over channels (pinned to the fp64 oracle <= 1e-6 RMS, "
@@ -302,7 +305,7 @@ def main():
     # STANDARD workloads do not hand the spectrum back (the reference's main.cpp never reads
     # it) unless --write-spec: the single launch (config 2) then consumes it on chip, the
     # split path still writes and re-reads every row (the handle's own buffer; for pitch > 1
-    # the bins no output bin reads are not analysed, zeros are stored in their slots).
+    # the bins no output bin reads are neither analysed, written nor read back).
     # REF_COMPAT fills the caller's 2N-bin rows, as kernel.cu does.
     want_spec = args.write_spec or compat
     spec_on_chip = bool(pv.single_launch) and not want_spec
@@ -358,8 +361,8 @@ def main():
     # the row slots the analysis writes per frame: all of them, or — no spectrum handed back,
     # pitch > 1, L = 1024 (config 4) — only the lane registers holding a bin some output bin
     # reads (pv_analysis.hip NA instantiations: 64 NA slots).  The roofline counts those for
-    # both halves — the bytes the algorithm moves; the synthesis still loads whole rows (the
-    # stale slots are no output bin's source), so its traffic exceeds that
+    # both halves — the bytes the algorithm moves; the synthesis loads the same slots
+    # (k_synthesis NR: 12 of 16 registers for pitch 1.5)
     B_full = B
     if not want_spec and not compat and not pv.single_launch and effect == PITCH_SHIFT and scale > 1.0 \
             and N // 2 == 1024 and layout == PV_SPEC_PACKED and hop_a == 512:
@@ -423,8 +426,8 @@ def main():
     # HBM bytes of the whole path per frame: input and output samples, plus the spectrum row
     # written and re-read when it goes through HBM (the split path); a single launch that keeps
     # the spectrum on chip moves only the samples (SURVEY §8(d) fused-mode bytes)
-    path_bytes_per_frame = 4 * hop_a + 4 * hop_s + (0 if spec_on_chip else 8 * B + 8 * B_read)
-    path_bytes = path_bytes_per_frame * C * frames * world * args.steps
+    path_bpf = path_bytes_per_frame(hop_a, hop_s, B, B_read, spec_on_chip)
+    path_bytes = path_bpf * C * frames * world * args.steps
 
     cpu = None
     # the CPU baseline is a rank-0, N = 1 figure (the contract's cpu_baseline): an N-rank run
@@ -455,7 +458,7 @@ def main():
             "diagnostic_build": diag,
             "lib_sources_sha": lib_sha,
             "path_hbm_frac": path_bytes / dt / 1e9 / HBM_PEAK_GBS,
-            "path_bytes_per_frame": path_bytes_per_frame,
+            "path_bytes_per_frame": path_bpf,
             "measured_ceiling": ceiling,
             "kernels": kernels,
             "kernel_timing": "block: one event pair around the timed loop" if block
@@ -473,6 +476,14 @@ def main():
 VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (dense) peak, MI355X_MICROARCH.md
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 PEAK_SCLK_GHZ = 2.4
+
+
+def path_bytes_per_frame(hop_a, hop_s, B, B_read, spec_on_chip):
+    """HBM bytes of the whole path per frame (the line's path_hbm_frac): the input and output
+    samples, plus the spectrum row written (B slots) and re-read (B_read) when it goes
+    through HBM; the single launch that keeps it on chip moves the samples only (SURVEY
+    §8(d) fused-mode bytes)."""
+    return 4 * hop_a + 4 * hop_s + (0 if spec_on_chip else 8 * B + 8 * B_read)
 
 
 def alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat, spec_written=True):
@@ -551,6 +562,9 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
         regime = json.load(open(regime_path)).get(wl, {})
     except (OSError, ValueError):
         regime = {}
+    if regime.get("clock_ghz"):  # the measured clock, whatever the static estimate's state
+        valu["measured_clock_ghz"] = float(regime["clock_ghz"])
+        valu["clock_source"] = regime.get("clock_source")
     try:
         isa = json.load(open(isa_path))
         ent = isa.get(wl, {}).get(kernel)
@@ -559,10 +573,8 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
             valu["issue_cycles_per_frame"] = cyc
             if isa.get("_sources_sha16") == kernel_sources_sha():
                 valu["issue_frac_at_peak_clock"] = cyc * frames / (SIMDS * t * PEAK_SCLK_GHZ * 1e9)
-                if regime.get("clock_ghz"):
-                    clk = float(regime["clock_ghz"])
-                    valu["measured_clock_ghz"] = clk
-                    valu["clock_source"] = regime.get("clock_source")
+                if valu["measured_clock_ghz"]:
+                    clk = valu["measured_clock_ghz"]
                     valu["issue_frac_at_measured_clock"] = cyc * frames / (SIMDS * t * clk * 1e9)
                 valu["issue_source"] = ("profiles/isa_static.json (static count of this build's loop, "
                                         "measured issue costs)")

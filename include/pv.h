@@ -4,7 +4,9 @@
  * Plain pointers and sizes only; every float / pv_float2 pointer handed to a compute
  * entry point is a DEVICE pointer (hipMalloc / torch CUDA tensor) on the handle's device,
  * and `stream` is a hipStream_t (NULL = the legacy default stream).  All calls are
- * asynchronous with respect to the host (graph-capturable: no allocation, no sync).
+ * asynchronous with respect to the host (graph-capturable: no allocation, no sync) — the
+ * one exception is pv_process(spec = NULL) on the split path, whose first call allocates
+ * the handle's own rows unless pv_reserve_spectrum did (under capture it refuses instead).
  *
  * Which reference interface each entry point replaces (reference @ /root/reference):
  *   pv_create        PhaseVocoder(int samples, Effect e, float scale, int hop)
@@ -39,6 +41,10 @@
  *   PV_SYN_LANEK=0       per-bin unwrap constants from LDS instead of per-lane registers
  *   PV_FUSED=0           the split path even where the q = 1 single launch applies
  *   PV_FUSED_FRAMES=F    frames per run of the q = 1 single launch
+ *   PV_FUSED_HALF=0      pitch 2 single launch: the MODE 3 gather and full-size inverse FFT
+ *                        instead of the half-size resynthesis of X^2/|X| (MODE 4)
+ *   PV_FUSED_BALANCE=0   single launch of one channel: uniform runs (no balanced F+1 runs)
+ *   PV_COMPAT_ANA_FRAMES=F  REF_COMPAT analysis run length (1..256, default 4)
  *   PV_RT_LAUNCH=direct  pv_rt_callback launches the kernel instead of replaying the graph
  */
 #ifndef PV_H
@@ -209,9 +215,16 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
  * be NULL when the caller does not want the spectrum: on the single launch (pv_info.
  * single_launch = 1) it is then computed and consumed on chip and not written (SURVEY §8(d)
  * fused mode); on the split path it goes through the handle's own buffer (max_channels x
- * max_frames rows, allocated by the first such call: PV_ERR_NOMEM if that fails).  Either
- * way, for pitch > 1 the bins no output bin reads (above about L / scale) may be left
- * unanalysed; the output is the same bits as with a spectrum buffer. */
+ * max_frames rows, zeroed, allocated by pv_reserve_spectrum or by the first such call:
+ * PV_ERR_NOMEM if that fails; a first call made while `stream` is being captured returns
+ * PV_ERR_ARG, since an allocation cannot be captured).  Either way, for pitch > 1 the bins
+ * no output bin reads (above about L / scale) may be left unanalysed and are not read; the
+ * output is the same bits as with a spectrum buffer. */
+/* allocate (once, zeroed) the handle's own spectrum rows that pv_process(spec = NULL) uses
+ * on the split path, so that such calls can then be captured into a graph; thread-safe; a
+ * no-op for a single-launch handle.  Not capturable itself (it allocates). */
+pv_status pv_reserve_spectrum(pv_handle* h);
+
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream);

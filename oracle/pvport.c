@@ -210,3 +210,129 @@ int pvr_port_std_process_batch(const float* x, long ldx, long n, int C, int N, i
 #endif
     return used;
 }
+
+/* ------------------------------------------------------------------ REF_COMPAT, fp32
+ * The reference's own path (kernel.cu:299-348 analysis, kernel.cu:352-432 resynthesis, the
+ * main.cpp:228-297 offline loop) as an fp32 CPU port — kernel.cu is fp32 throughout — timed
+ * as the REF_COMPAT line's cpu_baseline; pvref.c's pvr_compat_process (fp64) stays the
+ * checker and tests/test_oracle.py pins this port to it (<= 1e-6 RMS per sample):
+ *   cudaWindow (Hamming, phaseVocoder.h:85-89) + cufftShiftPadZeros (kernel.cu:25-32) into a
+ *   2N real frame; C2C 2N (kernel.cu:324-336) as the 2N-point real FFT (an N-point complex
+ *   FFT + split: the input is real) with bins N+1 .. 2N-1 the conjugate mirror; cudaMagFreq
+ *   (kernel.cu:101-109) sqrtf and atanf(y / x) over all 2N bins (the GPU computes and stores
+ *   them all too); cudaTimeScale's y-bug (kernel.cu:121-129); C2R N on bins 0 .. N/2
+ *   (kernel.cu:363-368) as an N/2-point complex inverse FFT; /N, swap halves, window
+ *   (kernel.cu:380, 393, 406); the running overlap-add (kernel.cu:111-119, main.cpp:279). */
+typedef struct {
+    int N, hop;
+    float *w, *fr, *xw, *y, *front, *back;
+    pvr_c32 *tw2, *tws2, *twi, *tws_s, *work, *X, *S, *Z;
+} cport_ctx;
+
+static void cport_init(cport_ctx* c, int N, int hop_div) {
+    const int L2 = N;       /* complex points of the 2N-point real FFT */
+    const int L = N / 2;    /* complex points of the N-point C2R */
+    c->N = N;
+    c->hop = N / hop_div;
+    c->w = (float*)malloc(sizeof(float) * N);
+    pvr_hamming_ref(N, c->w);
+    c->fr = (float*)malloc(sizeof(float) * N);
+    c->xw = (float*)calloc(2 * (size_t)N, sizeof(float));
+    c->y = (float*)malloc(sizeof(float) * N);
+    c->front = (float*)malloc(sizeof(float) * N);
+    c->back = (float*)calloc(N, sizeof(float));
+    const int t2 = pvr_fft_v3_applies(L2) ? pvr_fft_v3_table_size(L2) : L2 / 2;
+    c->tw2 = (pvr_c32*)malloc(sizeof(pvr_c32) * (size_t)(t2 > 1 ? t2 : 1));
+    if (pvr_fft_v3_applies(L2)) pvr_fft_v3_table(L2, c->tw2);
+    else pvr_fft_twiddles(L2, c->tw2);
+    c->tws2 = (pvr_c32*)malloc(sizeof(pvr_c32) * (L2 + 1));
+    pvr_split_twiddles(2 * N, c->tws2);
+    c->twi = (pvr_c32*)malloc(sizeof(pvr_c32) * (L / 2 > 1 ? L / 2 : 1));
+    pvr_fft_twiddles(L, c->twi);
+    c->tws_s = (pvr_c32*)malloc(sizeof(pvr_c32) * (L + 1));
+    pvr_split_twiddles(N, c->tws_s);
+    c->work = (pvr_c32*)malloc(sizeof(pvr_c32) * 2 * (size_t)L2);
+    c->X = (pvr_c32*)malloc(sizeof(pvr_c32) * (L2 + 1));
+    c->S = (pvr_c32*)malloc(sizeof(pvr_c32) * 2 * (size_t)N);  /* the 2N-bin {mag, phase} row */
+    c->Z = (pvr_c32*)malloc(sizeof(pvr_c32) * (L + 1));
+}
+
+static void cport_free(cport_ctx* c) {
+    free(c->w); free(c->fr); free(c->xw); free(c->y); free(c->front); free(c->back);
+    free(c->tw2); free(c->tws2); free(c->twi); free(c->tws_s); free(c->work); free(c->X);
+    free(c->S); free(c->Z);
+}
+
+static void cport_channel(cport_ctx* c, const float* x, long n, int frames, float* out) {
+    const int N = c->N, L = N / 2, hop = c->hop;
+    memset(c->back, 0, sizeof(float) * N);
+    for (int t = 0; t < frames; ++t) {
+        const long start = (long)t * hop;
+        for (int k = 0; k < N; ++k) c->fr[k] = (start + k < n) ? x[start + k] : 0.0f;
+        /* window + shift + zero pad (2N real samples, the middle N zeros stay zero) */
+        for (int k = 0; k < N / 2; ++k) {
+            c->xw[k] = c->fr[k + N / 2] * c->w[k + N / 2];
+            c->xw[k + N / 2 + N] = c->fr[k] * c->w[k];
+        }
+        pvr_rfft_c32(c->xw, 2 * N, c->tw2, c->tws2, c->X, c->work);
+        /* magnitude and atanf(y / x) of bins 0 .. N; bins N+1 .. 2N-1 mirror them */
+        for (int k = 0; k <= N; ++k) {
+            const float re = c->X[k].x, im = c->X[k].y;
+            c->S[k].x = sqrtf(re * re + im * im);
+            c->S[k].y = atanf(im / re);
+        }
+        for (int k = N + 1; k < 2 * N; ++k) { c->S[k].x = c->S[2 * N - k].x; c->S[k].y = -c->S[2 * N - k].y; }
+        /* cudaTimeScale (timeScale 1): x' = m cos(phi), y' = x' sin(phi); bins 0 .. N/2 */
+        for (int k = 0; k <= L; ++k) {
+            const float xr = c->S[k].x * cosf(c->S[k].y);
+            c->X[k].x = xr;
+            c->X[k].y = xr * sinf(c->S[k].y);
+        }
+        /* C2R N (Im of DC and Nyquist ignored): Z[k] = Fe + i Fo, L-point inverse FFT */
+        for (int k = 0; k < L; ++k) {
+            pvr_c32 A = c->X[k], Bc = c->X[L - k];
+            if (k == 0) { A.y = 0.0f; Bc.y = 0.0f; }
+            Bc.y = -Bc.y;
+            const float fer = A.x + Bc.x, fei = A.y + Bc.y;
+            const float dr = A.x - Bc.x, di = A.y - Bc.y;
+            const pvr_c32 tw = c->tws_s[k];
+            const float for_ = dr * tw.x + di * tw.y, foi = di * tw.x - dr * tw.y;
+            c->Z[k].x = fer - foi;
+            c->Z[k].y = fei + for_;
+        }
+        pvr_fft_c32(c->Z, c->work, L, c->twi, 1);
+        for (int m = 0; m < L; ++m) { c->y[2 * m] = c->Z[m].x; c->y[2 * m + 1] = c->Z[m].y; }
+        /* /N, swap halves, window; overlap-add with the running back frame, emit hop */
+        const float invN = 1.0f / (float)N;
+        for (int k = 0; k < N; ++k) c->front[k] = c->y[(k + L) % N] * invN * c->w[k];
+        for (int k = hop; k < N; ++k) c->front[k - hop] += c->back[k];
+        for (int j = 0; j < hop; ++j) out[start + j] = c->front[j];
+        memcpy(c->back, c->front, sizeof(float) * N);
+    }
+    for (int k = hop; k < N; ++k) out[(long)frames * hop + (k - hop)] = c->back[k];
+}
+
+int pvr_port_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
+                                  int frames, float* out, long ldo, int threads) {
+    int used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+        cport_ctx c;
+        cport_init(&c, N, hop_div);
+#pragma omp for schedule(dynamic, 1)
+        for (int ch = 0; ch < C; ++ch) cport_channel(&c, x + (size_t)ch * ldx, n, frames, out + (size_t)ch * ldo);
+        cport_free(&c);
+    }
+#else
+    (void)threads;
+    cport_ctx c;
+    cport_init(&c, N, hop_div);
+    for (int ch = 0; ch < C; ++ch) cport_channel(&c, x + (size_t)ch * ldx, n, frames, out + (size_t)ch * ldo);
+    cport_free(&c);
+#endif
+    return used;
+}

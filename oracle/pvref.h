@@ -121,6 +121,9 @@ int pvr_std_process_batch(const float* x, long ldx, long n, int C, int N, int ho
 int pvr_port_std_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
                                int effect, float scale, int frames, float* out, long ldo,
                                int threads);
+/* the fp32 CPU port of REF_COMPAT (oracle/pvport.c, the compat line's cpu_baseline) */
+int pvr_port_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
+                                  int frames, float* out, long ldo, int threads);
 /* REF_COMPAT (pvr_compat_process, the 4-argument constructor's Hamming) per channel */
 int pvr_compat_process_batch(const float* x, long ldx, long n, int C, int N, int hop_div,
                              int frames, float* out, long ldo, int threads);

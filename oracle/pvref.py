@@ -77,6 +77,8 @@ def lib():
         L.pvr_compat_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                                _f32p, c_long, c_int]
         L.pvr_compat_process_batch.restype = c_int
+        L.pvr_port_compat_process_batch.argtypes = L.pvr_compat_process_batch.argtypes
+        L.pvr_port_compat_process_batch.restype = c_int
         _lib = L
     return _lib
 
@@ -275,6 +277,21 @@ def compat_process_batch(x, N, hop_div, frames=None, threads=0):
     olen = frames * hop + (N - hop)
     out = np.zeros((C, olen), np.float32)
     used = lib().pvr_compat_process_batch(x, n, n, C, N, hop_div, frames, out, olen, int(threads))
+    return out, used
+
+
+def port_compat_process_batch(x, N, hop_div, frames=None, threads=0):
+    """The fp32 CPU port of REF_COMPAT (oracle/pvport.c): x [C, n] float32 -> (out [C, len]
+    float32, threads used).  The compat line's cpu_baseline; pinned to compat_process_batch
+    (the fp64 restatement) by the tests."""
+    x = _c32(x)
+    C, n = x.shape
+    hop = N // hop_div
+    if frames is None:
+        frames = num_frames(n, hop)
+    olen = frames * hop + (N - hop)
+    out = np.zeros((C, olen), np.float32)
+    used = lib().pvr_port_compat_process_batch(x, n, n, C, N, hop_div, frames, out, olen, int(threads))
     return out, used
 
 

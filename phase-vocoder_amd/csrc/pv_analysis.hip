@@ -27,8 +27,9 @@ constexpr int kAnaWaves1024 = 3;
 // profiles/r05_ab_ring.json; the code is kept out of the product as scripts/r05_ana_ring.patch.)
 constexpr int kAnaWG = 4;  // waves (runs) per workgroup
 
-// NA: lane registers analysed (Geo<L>::E = all; fewer: bins >= 64 NA not analysed, zeros in
-// their row slots — pv_process without a spectrum output, ana_run)
+// NA: lane registers analysed (Geo<L>::E = all; fewer: bins >= 64 NA not analysed and their
+// row slots not written — pv_process without a spectrum output, ana_run; the synthesis
+// reads only the written slots, k_synthesis NR)
 template <int L, bool EKL, int D, bool PACKED, int NA = Geo<L>::E>
 __global__ __launch_bounds__(64 * kAnaWG, (L < 512) ? 4 : (L == 512) ? kAnaWaves512 : (L == 1024) ? kAnaWaves1024 : 1) void k_std_analysis(AnaParams p) {
     using G_ = Geo<L>;

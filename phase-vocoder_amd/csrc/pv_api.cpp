@@ -106,8 +106,9 @@ void fft_table(int L, std::vector<float2>& t, bool v3 = false) {
 // d_tw_syn: the synthesis-side L-point table (stage-major or v3, fft_table), then at L = 1024
 // the v3 pass table of the batched synthesis's inverse FFT (k_synthesis reads tw + L; the
 // real-time and fused kernels run the analysis transform from the first table too), at
-// L = 256, 512 the L/2-point table of the fused pitch-2 resynthesis (k_fused MODE 4, tw + L)
-int tw_syn_len(int L) { return L == 1024 ? 2 * L : (L >= 256 ? L + L / 2 : L); }
+// L = 256, 512 the L/2-point table of the fused pitch-2 resynthesis (k_fused MODE 4, tw + L;
+// the single launch exists for L <= 512 only)
+int tw_syn_len(int L) { return L == 1024 ? 2 * L : (L == 256 || L == 512) ? L + L / 2 : L; }
 
 void split_twiddles(int N, std::vector<float2>& t) {
     t.resize(N / 2 + 1);
@@ -139,6 +140,10 @@ struct pv_handle {
     int N = 0, hop = 0, hs = 0, L_ana = 0, L_syn = 0, bins = 0, bins_pad = 0;
     int spec_bins = 0, spec_stride = 0, F = 16, tail_len = 0, max_runs = 0;
     int F_fused = 0;  // frames per run of the single-launch q = 1 path (0: not available)
+    // environment overrides, read once by pv_create (pv.h lists them)
+    int compat_ana_frames = 4;  // PV_COMPAT_ANA_FRAMES: REF_COMPAT analysis run length
+    int fused_half = 1;         // PV_FUSED_HALF=0: pitch 2 single launch without MODE 4
+    int fused_balance = 1;      // PV_FUSED_BALANCE=0: uniform runs on the single launch
     int src_hi = 0;   // highest analysis bin any output bin reads (pitch map; L otherwise)
     int tables_ready = 1;  // 0: pv_config.tables_external until pv_import_tables
     int mode = 0, effect = 0, pitch = 0, aligned_hop = 1, nan_faithful = 0;
@@ -156,8 +161,10 @@ struct pv_handle {
     int *d_runsum = nullptr, *d_carry = nullptr;
     float* d_tails = nullptr;
     // pv_process without a spectrum buffer on the split path: the handle's own rows
-    // (max_channels x max_frames, allocated at the first such call)
+    // (max_channels x max_frames, zeroed; allocated by pv_reserve_spectrum or the first such
+    // call outside a stream capture — spec_mu orders concurrent first calls)
     pv_float2* d_spec_own = nullptr;
+    std::mutex spec_mu;
     int* d_seam_flags = nullptr;  // fused path: per (channel, workgroup) arrival counters
 #ifdef PV_FUSED_STAMPS
     unsigned long long* d_stamps = nullptr;  // diagnostic build: per-wave phase stamps of k_fused
@@ -314,11 +321,7 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
         // writes in turn, and short runs (fewer rows written concurrently per channel, more
         // channels' rows in address order) stream faster (profiles/r05_ab_compat_F.txt);
         // the synthesis keeps h->F (its seams)
-        int fa = 4;
-        if (const char* ev = std::getenv("PV_COMPAT_ANA_FRAMES")) {
-            const int f = std::atoi(ev);
-            if (f >= 1 && f <= 256) fa = f;
-        }
+        const int fa = h->compat_ana_frames;
         p.F = fa;
         p.nruns = (frames + fa - 1) / fa;
     }
@@ -397,6 +400,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.tail_len = h->tail_len;
     p.k_lane = h->k_lane;
     p.packed = h->packed;
+    p.src_hi = h->src_hi;
     const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
     PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, smode, C, p, s));
     const int nwg = (nruns + 3) / 4;
@@ -451,8 +455,7 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     // pitch 2: the periodic half-size resynthesis (k_fused MODE 4); PV_FUSED_HALF=0 keeps the
     // MODE 3 gather and the full-size inverse FFT (tests compare the two)
     p.tw_half = (tw_syn_len(h->L_syn) == h->L_syn + h->L_syn / 2) ? h->d_tw_syn + h->L_syn : nullptr;
-    if (const char* eh = std::getenv("PV_FUSED_HALF"))
-        if (eh[0] == '0') p.tw_half = nullptr;
+    if (!h->fused_half) p.tw_half = nullptr;
     p.hs = h->hs;
     p.spec = reinterpret_cast<float2*>(spec);
     p.ld_spec = ld_spec;
@@ -468,7 +471,7 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     p.src_hi = h->src_hi;
     p.nwg = (nruns + 3) / 4;
     p.n4 = 0;
-    // one channel whose workgroups do not fill whole rounds of the 256 CUs (config 2: 862 =
+    // a stream whose workgroups do not fill whole rounds of the 256 CUs (config 2: 862 =
     // 3 x 256 + 94, so 94 CUs ran a 4th workgroup, 12 frames on their SIMDs against 9):
     // exactly `rounds` workgroups per CU, some runs one frame longer (k_fused "balanced";
     // PV_FUSED_BALANCE=0 turns it off).  The run boundaries move, so the seams' rounding
@@ -476,9 +479,10 @@ pv_status do_fused(pv_handle* h, const float* x, long long ldx, long long n, int
     {
         constexpr int kRoundCUs = 256;  // MI355X
         const int rounds = p.nwg / kRoundCUs;
-        const char* eb = std::getenv("PV_FUSED_BALANCE");
-        const bool on = !(eb && eb[0] == '0');
-        if (on && C == 1 && rounds >= 1 && p.nwg % kRoundCUs != 0) {
+        const bool on = h->fused_balance != 0;
+        // (decided from the frame count alone, for any number of channels: a channel's runs
+        // and so its output bits are the same alone or in a batch — ADVICE r5)
+        if (on && rounds >= 1 && p.nwg % kRoundCUs != 0) {
             const int G = rounds * kRoundCUs;
             const long long n4 = (long long)frames - 4LL * F * G;
             if (n4 > 0 && n4 <= 4LL * G) {
@@ -704,6 +708,13 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
                 if (cost_of[j] * 100 <= best * 102) F = f;
         }
     }
+    // the single-launch and REF_COMPAT overrides (pv.h), read once here
+    if (const char* ev = std::getenv("PV_COMPAT_ANA_FRAMES")) {
+        const int f = std::atoi(ev);
+        if (f >= 1 && f <= 256) h->compat_ana_frames = f;
+    }
+    if (const char* eh = std::getenv("PV_FUSED_HALF")) h->fused_half = (eh[0] == '0') ? 0 : 1;
+    if (const char* eb = std::getenv("PV_FUSED_BALANCE")) h->fused_balance = (eb[0] == '0') ? 0 : 1;
     // tuning override (even, 8..256): PV_RUN_FRAMES
     if (const char* ev = std::getenv("PV_RUN_FRAMES")) {
         const int f = std::atoi(ev);
@@ -900,6 +911,30 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
                           (hipStream_t)stream);
 }
 
+// the handle's own spectrum rows (split path, pv_process with spec = NULL): allocated and
+// zeroed once, under the handle's lock, so two threads' first calls allocate one buffer
+static pv_status reserve_spec_own(pv_handle* h) {
+    std::lock_guard<std::mutex> lk(h->spec_mu);
+    if (h->d_spec_own) return PV_OK;
+    const size_t bytes = sizeof(pv_float2) * (size_t)h->cfg.max_channels * (size_t)h->cfg.max_frames *
+                         (size_t)h->spec_stride;
+    pv_float2* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(PV_ERR_NOMEM, "spectrum rows of a spec = NULL call");
+    if (hipMemset(p, 0, bytes) != hipSuccess) {
+        (void)hipFree(p);
+        return fail(PV_ERR_HIP, "zeroing the spectrum rows of a spec = NULL call");
+    }
+    h->d_spec_own = p;
+    return PV_OK;
+}
+
+pv_status pv_reserve_spectrum(pv_handle* h) {
+    if (!h) return fail(PV_ERR_ARG, "null handle");
+    DeviceGuard g(h->cfg.device);
+    if (h->F_fused > 0) return PV_OK;  // the single launch keeps a spec = NULL spectrum on chip
+    return reserve_spec_own(h);
+}
+
 pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_samples,
                      int channels, int frames, pv_float2* spec, long long ld_spec, float* out,
                      long long ldo, void* stream) {
@@ -913,13 +948,17 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     // (pitch > 1) are not analysed
     int src_hi = -1;
     if (!spec && channels > 0 && frames > 0) {
-        if (!h->d_spec_own) {
-            const size_t bytes = sizeof(pv_float2) * (size_t)h->cfg.max_channels *
-                                 (size_t)h->cfg.max_frames * (size_t)h->spec_stride;
-            if (hipMalloc(&h->d_spec_own, bytes) != hipSuccess) {
-                h->d_spec_own = nullptr;
-                return fail(PV_ERR_NOMEM, "spectrum buffer of a spec = NULL call");
-            }
+        bool have;
+        {
+            std::lock_guard<std::mutex> lk(h->spec_mu);
+            have = h->d_spec_own != nullptr;
+        }
+        if (!have) {
+            // an allocation cannot be captured: under capture the rows must exist already
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+                return fail(PV_ERR_ARG, "pv_process(spec = NULL) under stream capture: call pv_reserve_spectrum first");
+            if ((st = reserve_spec_own(h)) != PV_OK) return st;
         }
         spec = h->d_spec_own;
         ld_spec = (long long)h->cfg.max_frames * h->spec_stride;
@@ -928,8 +967,8 @@ pv_status pv_process(pv_handle* h, const float* x, long long ldx, long long n_sa
     const bool std_mode = (h->mode == PV_MODE_STANDARD) && h->q > 1;  // run records feed the scan
     st = do_analysis(h, x, ldx, n_samples, channels, frames, spec, ld_spec, std_mode, s, src_hi);
     if (st != PV_OK) return st;
-    // (the synthesis reads whole rows: an instantiation reading only the analysed slots was
-    // 5 % slower on config 4, profiles/r05_ab_c4_skip.txt)
+    // (single-source pitch: the synthesis reads only the row slots of bins <= src_hi, the
+    // ones the analysis wrote, k_synthesis NR)
     return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, std_mode, s);
 }
 
@@ -966,7 +1005,7 @@ std::vector<TableSeg> table_segments(const pv_handle* h) {
 TableBlobHeader blob_header(const pv_handle* h) {
     TableBlobHeader hd{};
     hd.magic = kBlobMagic;
-    hd.version = 1;
+    hd.version = 2;  // 2: the L/2 synthesis table only at L = 256, 512 (tw_syn_len)
     hd.n_samps = h->N;
     hd.hop = h->hop;
     hd.hs = h->hs;
@@ -1172,6 +1211,9 @@ pv_status pv_rt_reset(pv_rt* rt, void* stream) {
 
 pv_status pv_rt_create(const pv_config* cfg, int channels, pv_rt** out) {
     if (!cfg || !out) return fail(PV_ERR_ARG, "null argument");
+    // the version first: no other field of a caller's struct is read before it matches
+    if (cfg->abi_version != PV_ABI_VERSION)
+        return fail(PV_ERR_ARG, "pv_config.abi_version != PV_ABI_VERSION (caller built against another pv.h)");
     if (cfg->tables_external) return fail(PV_ERR_UNSUPPORTED, "tables_external: batch handles only");
     *out = nullptr;
     if (cfg->mode != PV_MODE_STANDARD)
@@ -1404,6 +1446,9 @@ void pv_harmonizer_destroy(pv_harmonizer* hz) {
 
 pv_status pv_harmonizer_create(const pv_config* cfg, const float* ratios, int voices, pv_harmonizer** out) {
     if (!cfg || !ratios || !out) return fail(PV_ERR_ARG, "null argument");
+    // the version first: no other field of a caller's struct is read before it matches
+    if (cfg->abi_version != PV_ABI_VERSION)
+        return fail(PV_ERR_ARG, "pv_config.abi_version != PV_ABI_VERSION (caller built against another pv.h)");
     if (cfg->tables_external) return fail(PV_ERR_UNSUPPORTED, "tables_external: batch handles only");
     *out = nullptr;
     if (voices <= 0 || voices > 64) return fail(PV_ERR_ARG, "voices must be in [1, 64]");

@@ -127,7 +127,9 @@ __global__ __launch_bounds__(256, PV_FUSED_WAVES) void k_fused(FusedParams p) {
         const int k = blockIdx.x;
         const long long a = (long long)k * p.n4 / p.nwg, b = (long long)(k + 1) * p.n4 / p.nwg;
         const int m = (int)(b - a);
-        const int r = (int)((blockIdx.y * gridDim.x + blockIdx.x) >> 8) & 3;
+        // (the rotation follows blockIdx.x alone, so a channel's runs — and its output bits —
+        // do not depend on its position in the batch; for one channel it is the dispatch round)
+        const int r = (int)(blockIdx.x >> 8) & 3;
         int pre = 0;
         for (int v = 0; v < w; ++v) pre += p.F + ((((v - r) & 3) < m) ? 1 : 0);
         t0 = 4 * p.F * k + (int)a + pre;

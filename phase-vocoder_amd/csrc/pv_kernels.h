@@ -40,7 +40,8 @@ struct AnaParams {
     int nan_faithful;       // REF_COMPAT: x=y=0 -> NaN phase (kernel.cu:108)
     int packed;             // STANDARD rows in the PV_SPEC_PACKED layout (bin L in slot 0)
     int src_hi;             // STANDARD, L >= 1024: bins above it are not analysed (their row
-                            // slots get zeros) — pv_process without a spectrum output; L
+                            // slots are not written; the synthesis does not read them:
+                            // k_synthesis NR) — pv_process without a spectrum output; L
                             // otherwise
 };
 
@@ -80,6 +81,8 @@ struct SynParams {
     int tail_len;
     int k_lane;                        // e_k, (p j_k) mod q depend on k mod 64 only (syn_run LANEK)
     int packed;                        // PV_SPEC_PACKED rows (bins 0 and L in slot 0)
+    int src_hi;                        // highest analysis bin an output bin reads (single-
+                                       // source pitch: the row slots above it are not read)
 };
 
 // single-launch STANDARD path for q = 1 (pv_fused.hip)

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
 // (tests/test_abi.py checks both)
 constexpr int kSynWaves512 = 3;
 constexpr int kSynWaves1024 = 1;
-template <int L, int MODE, int DT, bool QPOW2 = false, bool LANEK = false>
+template <int L, int MODE, int DT, bool QPOW2 = false, bool LANEK = false, int NR = Geo<L>::E>
 __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (L == 1024) ? kSynWaves1024 : 1) void k_synthesis(SynParams p) {
     using G_ = Geo<L>;
     constexpr bool ROLA = DT > 0;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256, (L <= 256) ? 4 : (L == 512) ? kSynWaves512 : (
     }
     constexpr int NS = SynTraits<L, MODE, DT, QPOW2>::NS, D = SynTraits<L, MODE, DT, QPOW2>::D;
     float2 acc[NS];
-    syn_run<L, MODE, DT, QPOW2, LANEK>(
+    syn_run<L, MODE, DT, QPOW2, LANEK, NR>(
         p, SynCarve{twl, twsl, tiles, rings, gainl, ekl, jkl, srcl}, tw0, lane, w, c, t0, nfr, M, phprev, acc);
     if constexpr (ROLA) {
         // the run's tail (positions F*hs + j, j < N - hs) -> ring[j], over the tiles
@@ -421,6 +421,12 @@ hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// (A/B build: -DPV_SYN_FULLROWS reads whole rows for single-source pitch too)
+#ifdef PV_SYN_FULLROWS
+constexpr bool kSynFullRows = true;
+#else
+constexpr bool kSynFullRows = false;
+#endif
 // QPOW2 kernels (q a power of two <= 2^24: every STANDARD configuration with a power-of-two
 // hop) for all overlap-add variants; the generic-q path uses the LDS ring (DT = 0).
 template <int MODE, bool QP>
@@ -429,7 +435,13 @@ static hipError_t launch_synthesis_mode(int L, int dt, dim3 grid, const SynParam
     switch (dt) {                                                                                         \
         case 1: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 1, QP, KL_>), grid, dim3(256), syn_lds<LL_>(1), s, p); break; \
         case 2: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 2, QP, KL_>), grid, dim3(256), syn_lds<LL_>(2), s, p); break; \
-        case 4: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP, KL_>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
+        case 4:                                                                                           \
+            if constexpr (MODE == 3 && LL_ == 1024 && KL_ && !kSynFullRows) {                            \
+                /* single-source pitch (config 4): only the row slots of source bins <= src_hi */        \
+                if (p.src_hi < 512) { hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP, KL_, 8>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; } \
+                if (p.src_hi < 768) { hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP, KL_, 12>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; } \
+            }                                                                                             \
+            hipLaunchKernelGGL((k_synthesis<LL_, MODE, 4, QP, KL_>), grid, dim3(256), syn_lds<LL_>(4), s, p); break; \
         default: hipLaunchKernelGGL((k_synthesis<LL_, MODE, 0, QP>), grid, dim3(256), syn_lds<LL_>(0), s, p); break; \
     }
     // per-lane unwrap constants: register overlap-add STANDARD kernels (QP, MODE != 1)

@@ -242,7 +242,11 @@ struct SynTraits {
 // 64 a multiple of the hop divisor and q of 64 / hop divisor, checked by the host —
 // config 3 and 4): two registers (and bin L's j constant) instead of two LDS reads per bin
 // and frame.
-template <int L, int MODE, int DT, bool QPOW2, bool LANEK = false>
+// NR: row slots read per frame (lane registers i < NR, bins < 64 NR): every slot, or for a
+// pitch ratio > 1 only those some output bin takes its source from (src_hi) — the other slots
+// are never gathered, and without a spectrum output the analysis does not write them
+// (k_std_analysis NA): they stay zero in the registers, no load, no stale bytes read.
+template <int L, int MODE, int DT, bool QPOW2, bool LANEK = false, int NR = Geo<L>::E>
 __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, const float2 (&tw0)[Geo<L>::E],
                                         int lane, int w, int c, int t0, int nfr,
                                         int (&M)[Geo<L>::E + 1], float (&phprev)[Geo<L>::E + 1],
@@ -399,10 +403,14 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
         constexpr bool LATE = ROLA && L >= 1024 && MODE != 2;  // (MODE 2: 260 VGPRs, 1 wave/SIMD)
         const bool fast_st = ROLA && p.out_aligned && obase + (long long)p.F * hs <= p.out_len;
         (void)fast_st;
+        static_assert(NR == E || (MODE == 3 && NR < E), "partial rows: single-source pitch only");
         float2 sv[E + 1];  // spectrum row of the next frame, loaded one frame ahead
+#pragma unroll
+        for (int i = NR; i < E; ++i) sv[i] = make_float2(0.0f, 0.0f);
+        if (NR < E) sv[E] = make_float2(0.0f, 0.0f);
         auto load_row = [&](const float2* srow) {
             PV_FOR_BINS(E, lane, {
-                if (i < E || !packed) sv[i] = srow[k];
+                if (i < NR || (i == E && NR == E && !packed)) sv[i] = srow[k];
             })
         };
         if (nfr > 0) load_row(specc + (long long)t0 * p.spec_stride);

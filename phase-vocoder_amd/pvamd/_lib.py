@@ -120,6 +120,8 @@ def lib():
     L.pv_resynthesis.restype = i
     L.pv_process.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, vp]
     L.pv_process.restype = i
+    L.pv_reserve_spectrum.argtypes = [vp]
+    L.pv_reserve_spectrum.restype = i
     L.pv_export_tables.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), vp]
     L.pv_export_tables.restype = i
     L.pv_import_tables.argtypes = [vp, vp, ctypes.c_size_t, vp]

@@ -222,6 +222,11 @@ class PhaseVocoder:
                                       out.stride(0), self._stream(stream)), "pv_process")
         return out, spec
 
+    def reserve_spectrum(self):
+        """Allocate (once, zeroed) the handle's own spectrum rows that process(spectrum=False)
+        uses on the split path, so that such calls can be captured into a graph."""
+        self._call(self._L.pv_reserve_spectrum(self._h), "pv_reserve_spectrum")
+
     # -------------------------------------------------------------- reference per-frame API
     def analysis_CUFFT(self, input, output, fft=None, intermediary=None):
         """PhaseVocoder::analysis_CUFFT (phaseVocoder.cpp:25-33): one frame of nSamps

@@ -1,6 +1,6 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-AB_STEPS=20 bash scripts/ab.sh old base:PV_RUN_FRAMES=72
+STEPS="tests c3 c4 c2 compat prof prof_c4" bash scripts/round_evidence.sh || exit $?
+AB_STEPS=20 AB_ARGS="--workload c4" bash scripts/ab.sh synfull || exit $?
+PV_LIB_PATH=$PWD/phase-vocoder_amd/build/variants/libpv_stamps.so timeout -k 10 120 python scripts/fused_stamps.py > gpurun_out/r06_c2_stamps.json || exit $?
+echo all done

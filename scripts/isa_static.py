@@ -33,7 +33,7 @@ KERNELS = {
     # config 4 (bench.py: no spectrum handed back, pitch 1.5): the instantiation analysing
     # lane registers 0 .. 11 (bins < 768; 12 square roots, no bin L)
     ("c4", "analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv14k_std_analysisILi1024ELb0ELi4ELb1ELi12E", 12),
-    ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1E", 33),
+    ("c4", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi1024ELi3ELi4ELb1ELb1ELi12E", 33),
     ("compat", "compat_analysis"): ("pv_analysis.hip", ["-fno-slp-vectorize"], "_ZN2pv17k_compat_analysisILi512E", 9),
     ("compat", "synthesis"): ("pv_kernels.hip", [], "_ZN2pv11k_synthesisILi512ELi1ELi2ELb0ELb0E", 17),
     # config 2's single launch (pitch 2: MODE 4, the half-size resynthesis of X^2 / |X|):

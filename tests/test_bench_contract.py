@@ -147,6 +147,36 @@ def test_committed_regime_evidence():
         assert os.path.exists(os.path.join(ROOT, "profiles", src))
 
 
+def test_path_bytes_count_hbm_bytes_only():
+    """path_hbm_frac counts the bytes that go through HBM: the split path
+    writes and re-reads the spectrum rows, the single launch (config 2) keeps them on chip."""
+    # config 3: 1 KiB in, 512 B out, a packed 4 KiB row written and re-read
+    assert bench.path_bytes_per_frame(256, 128, 512, 512, False) == 4 * 256 + 4 * 128 + 8 * 512 * 2
+    # config 2 on the single launch: the samples only (4 hop_a + 4 hop_s)
+    assert bench.path_bytes_per_frame(256, 256, 512, 512, True) == 2048
+
+
+def test_committed_c2_regime_evidence():
+    """The config-2 single launch's regime is stated with evidence: the
+    clock measured on c2 steps and the latency evidence of its per-wave stamps, so the bench
+    line's roofline carries both."""
+    import json
+    reg = json.load(open(os.path.join(ROOT, "profiles", "regime.json")))
+    c2 = reg["c2"]
+    assert 1.5 < c2["clock_ghz"] <= 2.4 and "stamps" in c2["clock_source"]
+    ev = c2["fused"]["latency_evidence"]
+    assert ev["launch_span_us"] > 0 and ev["sources"]
+    for src in ev["sources"].split(", "):
+        assert os.path.exists(os.path.join(ROOT, src.split(" ")[0])), src
+    N, hop, hs, B, frames = 1024, 256, 256, 512, 1722
+    sha = bench.kernel_sources_sha()
+    r = bench.roofline("fused", 0.023, "c2", N, hop, hs, B, frames, False, None, spec_written=False)
+    assert r["valu"]["measured_clock_ghz"] == c2["clock_ghz"]
+    if r["bound"] == "latency":
+        assert r["latency_evidence"] == ev
+    del sha
+
+
 def test_committed_isa_static_matches_sources():
     """profiles/isa_static.json must describe this build's kernels (regenerate it with
     scripts/isa_static.py after a kernel change)."""

@@ -84,7 +84,8 @@ def test_fused_equals_split_path(cuda, monkeypatch, N, hop_div, effect, scale):
     out_e, _, _ = _kernels(pe, xd)
     if half:
         assert np.abs(out_e.cpu().numpy() - gs).max() <= 1e-6
-        monkeypatch.setenv("PV_FUSED_HALF", "0")
+        monkeypatch.setenv("PV_FUSED_HALF", "0")  # read by pv_create: a new handle
+        pe = PhaseVocoder(N, effect, scale, hop_div, mode=STANDARD, max_channels=C, max_frames=frames)
         out_e, _, _ = _kernels(pe, xd)
     assert np.array_equal(out_e.cpu().numpy().view(np.uint32), gs.view(np.uint32))
 
@@ -165,8 +166,24 @@ def test_fused_balanced_runs(cuda, monkeypatch, seconds):
     ref = pvref.std_process(x, 1024, 4, ord("p"), 2.0)
     assert g.shape == ref.shape and np.isfinite(g).all()
     assert rms(g, ref) <= RMS_TOL
-    monkeypatch.setenv("PV_FUSED_BALANCE", "0")
+    monkeypatch.setenv("PV_FUSED_BALANCE", "0")  # read by pv_create: a new handle
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=pv_frames(n))
     out0, _ = pv.process(to_dev(x), spectrum=False)
     assert float((out0 - out).abs().max()) <= 1e-6
     again, _ = pv.process(to_dev(x), spectrum=False)  # deterministic
     assert torch.equal(again, out0)
+
+
+def test_fused_balanced_runs_same_bits_alone_or_batched(cuda):
+    """The balanced run split is decided from the frame count alone: a stream long
+    enough to take it gives the same output bits processed alone and as either channel of a
+    two-channel batch."""
+    import torch
+    n = int(37.3 * 44100)
+    x0, x1 = synth(n, 20241), synth(n, 20242)
+    pv1 = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=pv_frames(n))
+    alone0, _ = pv1.process(to_dev(x0), spectrum=False)
+    alone1, _ = pv1.process(to_dev(x1), spectrum=False)
+    pv2 = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_channels=2, max_frames=pv_frames(n))
+    both, _ = pv2.process(to_dev(np.stack([x0, x1])), spectrum=False)
+    assert torch.equal(both[0], alone0[0]) and torch.equal(both[1], alone1[0])

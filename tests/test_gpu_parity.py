@@ -373,3 +373,48 @@ def test_nonfinite_burst_recovers(cuda, effect, scale):
     # and before the burst too
     first_bad = 20000 // hop - N // hop
     assert rms(g[:max(first_bad, 0) * hs], ref[:max(first_bad, 0) * hs]) <= RMS_TOL
+
+
+def test_spec_null_rows_reserved_for_graph_capture(cuda):
+    """pv_process(spec = NULL) on the split path allocates the handle's own rows at its first
+    call: under a stream capture that first call is refused (no allocation is
+    captured), after pv_reserve_spectrum the same call captures, and the graph's replay gives
+    the uncaptured call's bits."""
+    import ctypes
+    import torch
+    from pvamd import _lib
+    x = synth(30000, 5)
+    xd = to_dev(x)
+    mk = lambda: PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_frames=200)
+    ref_pv = mk()
+    assert not ref_pv.single_launch
+    ref, _ = ref_pv.process(xd, spectrum=False)  # first call outside a capture: allocates
+    pv = mk()
+    frames = pv.num_frames(len(x))
+    out = pv.alloc_out(1, frames)
+    L = _lib.lib()
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+
+    def call():
+        return L.pv_process(pv._h, xd.data_ptr(), xd.numel(), len(x), 1, frames, None, 0, out.data_ptr(),
+                            out.stride(0), ctypes.c_void_p(s.cuda_stream))
+
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        st = call()
+        g.capture_end()
+    assert st == _lib.PV_ERR_ARG and b"pv_reserve_spectrum" in L.pv_last_error()
+    pv.reserve_spectrum()
+    pv.reserve_spectrum()  # idempotent
+    out.zero_()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        g2.capture_begin()
+        st = call()
+        g2.capture_end()
+    assert st == _lib.PV_OK
+    g2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

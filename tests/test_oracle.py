@@ -346,3 +346,17 @@ def test_fp32_port_pinned_to_oracle(N, effect, scale):
     assert got.shape == ref.shape and used >= 1
     err = np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2, axis=1))
     assert err.max() <= 1e-6, err
+
+
+@pytest.mark.parametrize("N,hop_div", [(1024, 4), (256, 2), (512, 4), (2048, 4)])
+def test_fp32_compat_port_pinned_to_oracle(N, hop_div):
+    """The fp32 CPU port of REF_COMPAT (oracle/pvport.c: kernel.cu's path in fp32, bench.py's
+    compat cpu_baseline) computes the fp64 restatement's output: <= 1e-6 RMS per sample on
+    every channel."""
+    import bench
+    x = bench.synth_channels_np(3, 44100 * 2, 20240)
+    ref, _ = pvref.compat_process_batch(x, N, hop_div, None, 2)
+    got, used = pvref.port_compat_process_batch(x, N, hop_div, None, 2)
+    assert got.shape == ref.shape and used >= 1
+    err = np.sqrt(np.mean((got.astype(np.float64) - ref.astype(np.float64)) ** 2, axis=1))
+    assert err.max() <= 1e-6, err
