@@ -544,9 +544,12 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
     profiles/isa_static.json, used only when its source hash matches this build) as a
     fraction of the SIMD cycles the launch had, at the 2.4 GHz peak clock and at the clock
     the chip was measured to hold on this workload (profiles/regime.json: the 1400 W cap
-    holds ~1.85 GHz on config 3).  `bound` is "hbm" or "valu" when that roof's fraction
-    exceeds BIND_FRAC, else "latency" — then `latency_evidence` carries the timing-only
-    ablations that place the kernel's time (profiles/regime.json)."""
+    holds ~1.8 GHz on config 3).  `bound` is "hbm" when the HBM fraction exceeds BIND_FRAC;
+    else "power" when the package was measured at its power cap on this workload
+    (`power_evidence`: the clock it holds there, the zero-data and ablation runs); else
+    "valu" above BIND_FRAC of the issue, else "latency" — with "latency" and "power",
+    `latency_evidence` carries the timing-only ablations that place the kernel's time
+    (profiles/regime.json)."""
     t = avg_ms * 1e-3
     alg_bytes = alg_bytes_per_frame(kernel, N, hop_a, hop_s, B, compat, spec_written) * frames
     achieved = alg_bytes / t / 1e9
@@ -586,8 +589,15 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
     if issue is None:
         issue = valu["issue_frac_at_peak_clock"]
     vfrac = max(valu["flop_frac"], issue or 0.0)
+    # the package power cap (profiles/regime.json: the power measured on this workload at the
+    # cap, with the clock it holds there): below the HBM roof the cap, not a roof, sets the
+    # time — the measured clock is what the issue fraction above is priced at
+    pw, cap = regime.get("package_power_w"), regime.get("power_cap_w")
+    power_capped = bool(pw and cap and float(pw) >= 0.99 * float(cap))
     if hbm_frac > BIND_FRAC and hbm_frac >= vfrac:
         bound = "hbm"
+    elif power_capped:
+        bound = "power"
     elif vfrac > BIND_FRAC:
         bound = "valu"
     else:
@@ -596,8 +606,10 @@ def roofline(kernel, avg_ms, wl, N, hop_a, hop_s, B, frames, compat, traffic,
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
            "frac_of": "hbm (the metric's % HBM roofline)", "traffic": traffic,
            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms, "valu": valu}
-    if bound == "latency":
+    if bound in ("latency", "power"):
         out["latency_evidence"] = (regime.get(kernel) or {}).get("latency_evidence")
+    if bound == "power":
+        out["power_evidence"] = (regime.get(kernel) or {}).get("power_evidence")
     return out
 
 

@@ -85,7 +85,8 @@ def test_compat_oracle_batch_and_baseline():
 def test_roofline_reports_both_roofs(tmp_path):
     """the line carries the HBM and the VALU roof of the dominant kernel and
     names the regime: "hbm" / "valu" when that roof's fraction exceeds bench.BIND_FRAC,
-    otherwise "latency" with the ablation evidence of profiles/regime.json."""
+    "power" when the workload was measured at the package power cap, otherwise "latency"
+    with the ablation evidence of profiles/regime.json."""
     import json
     N, hop, hs, B, frames = 1024, 256, 128, 512, 1024 * 1722
     regime = tmp_path / "regime.json"
@@ -133,6 +134,20 @@ def test_roofline_reports_both_roofs(tmp_path):
     r5 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file("0", 4000.0), **kw)
     assert "STALE" in r5["valu"]["issue_source"] and r5["valu"]["issue_frac_at_peak_clock"] is None
     assert r5["bound"] == "latency"
+    # a workload measured at the package power cap: "power", with its evidence, below the
+    # HBM roof whatever the issue fraction
+    regime2 = tmp_path / "regime2.json"
+    regime2.write_text(json.dumps({"c3": {"clock_ghz": 1.79, "clock_source": "test", "package_power_w": 1400,
+                                          "power_cap_w": 1400,
+                                          "analysis": {"latency_evidence": {"memory_side_ms": 1.86},
+                                                       "power_evidence": {"clock_ghz": 1.79}}}}))
+    kw2 = dict(regime_path=str(regime2))
+    for cyc in (1600.0, 2400.0):
+        r6 = bench.roofline("analysis", 2.0, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file(sha, cyc), **kw2)
+        assert r6["bound"] == "power" and r6["power_evidence"] == {"clock_ghz": 1.79}
+        assert r6["latency_evidence"] == {"memory_side_ms": 1.86}
+    r7 = bench.roofline("analysis", 1.2, "c3", N, hop, hs, B, frames, False, None, isa_path=isa_file(sha, 100.0), **kw2)
+    assert r7["bound"] == "hbm"
 
 
 def test_committed_regime_evidence():
@@ -141,7 +156,11 @@ def test_committed_regime_evidence():
     import json
     reg = json.load(open(os.path.join(ROOT, "profiles", "regime.json")))
     ev = reg["c3"]["analysis"]["latency_evidence"]
-    assert 1.5 < reg["c3"]["clock_ghz"] < 2.4 and "r04_clock_power_c3" in reg["c3"]["clock_source"]
+    assert 1.5 < reg["c3"]["clock_ghz"] < 2.4 and "r06_clock_power_c3" in reg["c3"]["clock_source"]
+    assert reg["c3"]["package_power_w"] >= 0.99 * reg["c3"]["power_cap_w"]
+    pe = reg["c3"]["analysis"]["power_evidence"]
+    for src in pe["sources"].split(", "):
+        assert os.path.exists(os.path.join(ROOT, src)), src
     assert ev["memory_side_ms"] > 0 and "r04_ab_c3_ablation" in ev["sources"]
     for src in ("r04_ab_c3_ablation.txt", "r05_mix_probe.jsonl", "r05_ab_ring.json"):
         assert os.path.exists(os.path.join(ROOT, "profiles", src))
