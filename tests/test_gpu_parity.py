@@ -32,7 +32,11 @@ def rms(a, b):
     return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
 
 
-@pytest.mark.parametrize("N,hop_div", [(1024, 4), (2048, 4), (512, 4), (256, 4), (1024, 2), (2048, 8)])
+# (the analysis's frame-loop forms: 1024/4, 512/4, 1024/2, 512/2 the register rotation in
+# groups of 4 / 4 / 2 / 2 frames; 1024/8 and 256/4 the mirrored pairs without it; 2048/* the
+# L = 1024 per-bin split)
+@pytest.mark.parametrize("N,hop_div", [(1024, 4), (2048, 4), (512, 4), (256, 4), (1024, 2), (2048, 8),
+                                       (512, 2), (1024, 8)])
 def test_std_analysis_bit_exact(cuda, N, hop_div):
     x = synth(20 * N, 7)
     pv = PhaseVocoder(N, TIME_SHIFT, 1.0, hop_div, mode=STANDARD, max_frames=1000)
