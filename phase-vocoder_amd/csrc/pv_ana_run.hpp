@@ -371,9 +371,13 @@ __device__ __forceinline__ void ana_run(const AnaParams& p, const AnaLds& lt, fl
             // register (q + D r) mod E, so its D new pairs land in the registers frame u + r - 1
             // no longer needs and no register is shifted (the shifting form costs 2 (E - D)
             // v_mov per frame); the groups end at rotation 0, where the loop below continues.
-            // (L <= 512 with groups of at most 4 frames: longer unrolled groups blow up the
-            // compile, and the L = 1024 kernels sit at their VGPR bound)
-            if constexpr (E % D == 0 && E / D <= 4 && L <= 512) {
+            // (groups of at most 4 frames: longer unrolled groups blow up the compile)
+            // (L = 1024 only with packed rows and at most 12 lane registers analysed — config 4
+            // without a spectrum output, 163 VGPRs: with all 16, or natural rows, the rotated
+            // loop spills at its 168-VGPR bound; config 4's analysis -4.9 %,
+            // profiles/r06_ab_c4_analysis_rot.txt)
+            constexpr bool ROT_FITS = L <= 512 || (L == 1024 && NA <= 12 && PACKED);
+            if constexpr (E % D == 0 && E / D <= 4 && ROT_FITS) {
                 constexpr int RR = E / D;
                 const int umain = ufast - ufast % RR;
                 auto window_rot = [&](auto rc) {
