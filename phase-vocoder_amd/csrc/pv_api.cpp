@@ -920,7 +920,9 @@ static pv_status reserve_spec_own(pv_handle* h) {
                          (size_t)h->spec_stride;
     pv_float2* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return fail(PV_ERR_NOMEM, "spectrum rows of a spec = NULL call");
-    if (hipMemset(p, 0, bytes) != hipSuccess) {
+    // (synchronised: the caller's stream may be a non-blocking one, which the null stream's
+    // memset would not order before the first analysis)
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(p);
         return fail(PV_ERR_HIP, "zeroing the spectrum rows of a spec = NULL call");
     }
