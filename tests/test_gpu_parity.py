@@ -422,3 +422,16 @@ def test_spec_null_rows_reserved_for_graph_capture(cuda):
     g2.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_reserve_spectrum_on_single_launch_is_a_no_op(cuda):
+    """A single-launch handle (q = 1: pitch 2.0) keeps a spec = NULL spectrum on chip, so
+    pv_reserve_spectrum allocates nothing and a capture of its pv_process needs no reserve."""
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 2.0, 4, mode=STANDARD, max_frames=200)
+    assert pv.single_launch
+    pv.reserve_spectrum()
+    x = to_dev(synth(30000, 6))
+    out, spec = pv.process(x, spectrum=False)
+    assert spec is None
+    ref = pvref.std_process(synth(30000, 6), 1024, 4, ord("p"), 2.0)
+    assert rms(out.cpu().numpy()[0], ref) <= RMS_TOL
