@@ -261,7 +261,8 @@ pv_status pv_rt_callback(pv_rt* rt, const float* in, float* out);
  * and one unwrap scan (cfg: STANDARD; effect and scale are ignored).  voices_out[k*ld_voice
  * + c*ldo + i], i < pv_output_length (every voice has out_hop = hop); each voice equals
  * pv_process() with its ratio.  mix (nullable): mix[c*ld_mix + i] = sum_k gains[k] * voice
- * k (gains: host array of K floats).  At most 64 voices. */
+ * k (gains: host array of K floats).  spec (required) receives the shared analysis, as
+ * pv_process's.  At most 64 voices.  channels or frames 0: nothing is done (PV_OK). */
 typedef struct pv_harmonizer pv_harmonizer;
 pv_status pv_harmonizer_create(const pv_config* cfg, const float* ratios, int voices, pv_harmonizer** out);
 void pv_harmonizer_destroy(pv_harmonizer* hz);

@@ -1480,12 +1480,13 @@ pv_status pv_harmonize(pv_harmonizer* hz, const float* x, long long ldx, long lo
     pv_handle* h0 = hz->voices[0];
     pv_status st = check_common(h0, channels, frames);
     if (st != PV_OK) return st;
+    if (mix && !gains) return fail(PV_ERR_ARG, "mix needs gains");
+    if (channels == 0 || frames == 0) return PV_OK;  // nothing to do (as pv_process)
     if (!voices_out) return fail(PV_ERR_ARG, "null voices_out");
     const int K = (int)hz->voices.size();
     const long long olen = pv_output_length(h0, frames);
     if (K > 1 && ld_voice < (long long)(channels - 1) * ldo + olen)
         return fail(PV_ERR_ARG, "ld_voice smaller than one voice's output block");
-    if (mix && !gains) return fail(PV_ERR_ARG, "mix needs gains");
     DeviceGuard g(h0->cfg.device);
     hipStream_t s = (hipStream_t)stream;
     st = do_analysis(h0, x, ldx, n_samples, channels, frames, spec, ld_spec, true, s);

@@ -211,3 +211,36 @@ def test_device_asm_has_no_prefetch_or_scc_hazards(device_asm):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "prefetch_hazards.py"), *outs],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("0 hazard(s)"), r.stdout[-3000:]
+
+
+def test_rt_and_harmonizer_create_reject_bad_configs_without_touching_gpu():
+    """pv_rt_create / pv_harmonizer_create check the ABI version before any other field
+    (ADVICE r5), then their own limits, all before a device call (pv_api.cpp)."""
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    ratios = (ctypes.c_float * 2)(1.5, 0.5)
+    good = _lib.config(1024, 4, ord("p"), 1.5, 1, 1, 10, 0)
+    bad_abi = _lib.config(1024, 4, ord("p"), 1.5, 1, 1, 10, 0)
+    bad_abi.abi_version = 4
+    assert L.pv_rt_create(ctypes.byref(bad_abi), 2, ctypes.byref(h)) == _lib.PV_ERR_ARG
+    assert b"abi_version" in L.pv_last_error()
+    assert L.pv_harmonizer_create(ctypes.byref(bad_abi), ratios, 2, ctypes.byref(h)) == _lib.PV_ERR_ARG
+    assert b"abi_version" in L.pv_last_error()
+    # voice count outside [1, 64]
+    for k in (0, -1, 65):
+        assert L.pv_harmonizer_create(ctypes.byref(good), ratios, k, ctypes.byref(h)) == _lib.PV_ERR_ARG
+        assert not h.value
+    # both run the STANDARD pipeline only; neither takes external tables
+    compat = _lib.config(1024, 4, ord("t"), 1.0, 0, 1, 10, 0)
+    assert L.pv_harmonizer_create(ctypes.byref(compat), ratios, 2, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
+    assert L.pv_rt_create(ctypes.byref(compat), 2, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
+    ext = _lib.config(1024, 4, ord("p"), 1.5, 1, 1, 10, 0, tables_external=1)
+    assert L.pv_harmonizer_create(ctypes.byref(ext), ratios, 2, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
+    assert L.pv_rt_create(ctypes.byref(ext), 2, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
+    # real time: natural rows only, at least one channel
+    packed = _lib.config(1024, 4, ord("p"), 1.5, 1, 1, 10, 0, spec_layout=1)
+    assert L.pv_rt_create(ctypes.byref(packed), 2, ctypes.byref(h)) == _lib.PV_ERR_UNSUPPORTED
+    assert L.pv_rt_create(ctypes.byref(good), 0, ctypes.byref(h)) == _lib.PV_ERR_ARG
+    assert not h.value
+    # null harmoniser
+    assert L.pv_harmonize(None, None, 0, 0, 1, 1, None, 0, None, 0, 0, None, None, 0, None) == _lib.PV_ERR_ARG

@@ -47,3 +47,46 @@ def test_harmonizer_voices_and_mix(cuda, monkeypatch, N, ratios):
         assert rms(v[k][1], ref) <= RMS_TOL
     want = sum(g * v[k].astype(np.float64) for k, g in enumerate(gains))
     assert np.max(np.abs(mix.cpu().numpy() - want)) <= 1e-6
+
+
+def test_harmonizer_spectrum_is_the_single_voice_spectrum(cuda, monkeypatch):
+    """The shared analysis writes the same rows, bit for bit, as a PhaseVocoder of the
+    first voice's ratio (same contract, same kernels)."""
+    import torch
+    monkeypatch.setenv("PV_FUSED", "0")
+    C = 2
+    xs = np.stack([synth(30000, 90 + c) for c in range(C)])
+    hz = Harmonizer(1024, [1.5, 0.75], 4, max_channels=C, max_frames=300)
+    _, mix, spec = hz.harmonize(torch.from_numpy(xs).cuda())
+    assert mix is None
+    pv = PhaseVocoder(1024, PITCH_SHIFT, 1.5, 4, mode=STANDARD, max_channels=C, max_frames=300)
+    _, spec1 = pv.process(torch.from_numpy(xs).cuda())
+    a, b = spec.cpu().numpy(), spec1.cpu().numpy()
+    bins = 1024 // 2 + 1
+    assert np.array_equal(a[:, :, :bins].view(np.uint32), b[:, :, :bins].view(np.uint32))
+
+
+def test_harmonizer_mix_with_exact_gains(cuda):
+    """Gains 2 and 0: the mix is exactly twice voice 0 (a power-of-two scale and an added
+    +0 round nothing)."""
+    import torch
+    xs = synth(25000, 95)[None, :]
+    hz = Harmonizer(512, [1.25, 2.0], 4, max_channels=1, max_frames=300)
+    voices, mix, _ = hz.harmonize(torch.from_numpy(xs).cuda(), gains=[2.0, 0.0])
+    v = voices.cpu().numpy()
+    assert np.isfinite(v).all() and np.abs(v[0]).max() > 1e-3
+    assert np.array_equal(mix.cpu().numpy(), 2.0 * v[0])
+
+
+def test_harmonizer_single_voice_and_empty_input(cuda):
+    import torch
+    x = torch.from_numpy(synth(20000, 97)[None, :]).cuda()
+    hz = Harmonizer(1024, [1.5], 4, max_channels=1, max_frames=200)
+    voices, mix, _ = hz.harmonize(x, gains=[1.0])
+    assert voices.shape[0] == 1
+    assert np.array_equal(mix.cpu().numpy(), voices[0].cpu().numpy())
+    ref = pvref.std_process(synth(20000, 97), 1024, 4, ord("p"), 1.5)
+    assert rms(voices[0, 0].cpu().numpy(), ref) <= RMS_TOL
+    # fewer samples than one hop: no frames, empty outputs, no error
+    voices, mix, spec = hz.harmonize(x[:, :100], gains=[1.0])
+    assert voices.numel() == 0 and mix.numel() == 0 and spec.shape[1] == 0
