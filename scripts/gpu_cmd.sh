@@ -1,4 +1,4 @@
 set -u
 mkdir -p gpurun_out
-STEPS="tests c3 c2 c4 compat rt prof prof_c4 prof_c2 prof_compat" bash scripts/round_evidence.sh || exit $?
-echo all done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_rt.py tests/test_gpu_harmonizer.py -m gpu -x -q -rf --timeout 120 --timeout-method thread -k "geometries or rt_stream or harmonizer" > gpurun_out/pytest_new.log 2>&1; rc=$?
+tail -15 gpurun_out/pytest_new.log; exit $rc

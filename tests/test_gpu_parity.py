@@ -240,6 +240,13 @@ def test_ragged_channel_strides_and_determinism(cuda):
     (2048, 8, PITCH_SHIFT, 1.25),  # L=1024, out hop 256 (DT = 2)
     (1024, 4, PITCH_SHIFT, 1.0),   # L=512
     (1024, 3, PITCH_SHIFT, 1.5),   # L=512, hop 341: LDS ring overlap-add (DT = 0)
+    # output-phase ratios whose denominator q is not a power of two (hop not one): the
+    # generic modular path (M mod q, (t + 1) mod q), which the power-of-two kernels skip
+    (1024, 3, TIME_SHIFT, 0.5),    # hop 341, out hop 170: q = 341
+    (512, 3, TIME_SHIFT, 1.37),    # hop 170, out hop 232: q = 85, stretch > 1
+    (2048, 6, TIME_SHIFT, 0.8),    # L=1024, hop 341, out hop 272: q = 341
+    (256, 3, TIME_SHIFT, 1.5),     # L=128, hop 85, out hop 127: q = 85
+    (1024, 4, TIME_SHIFT, 0.25),   # out hop 64: q = 4, LDS ring
 ])
 def test_std_process_parity_geometries(cuda, N, hop_div, effect, scale):
     """Both overlap-add paths (registers when the out hop is a multiple of 128 and

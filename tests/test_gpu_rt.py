@@ -45,6 +45,8 @@ def oracle_stream(x, N, hop_div, effect, scale, K):
     (512, 4, TIME_SHIFT, 1.5, 1),      # out hop 192 (not a multiple of 64)
     (2048, 4, PITCH_SHIFT, 2.0, 4),    # L = 1024 instantiation
     (1024, 2, PITCH_SHIFT, 0.75, 5),
+    (1024, 3, TIME_SHIFT, 0.5, 2),     # hop 341, out hop 170: q = 341 (generic modular path)
+    (512, 3, TIME_SHIFT, 1.37, 1),     # hop 170, out hop 232: q = 85
 ])
 def test_rt_stream_matches_oracle(cuda, N, hop_div, effect, scale, per_push):
     import torch
