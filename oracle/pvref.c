@@ -666,6 +666,15 @@ int pvr_compat_process(const float* x, long n, int N, int hop_div, int frames, d
 
 int pvr_compat_process_ex(const float* x, long n, int N, int hop_div, int frames,
                           const float* window, int nan_faithful, double* out) {
+    return pvr_compat_process_hs(x, n, N, hop_div, N / hop_div, frames, window, nan_faithful, out);
+}
+
+/* out hop hs = (int)(timeScale * hop) (phaseVocoder.h:74): the reference passes outHopSize to
+ * resynthesis_CUFFT (phaseVocoder.cpp:68) while cudaTimeScale's factor is hard-coded 1
+ * (kernel.cu:354), so a time scale only moves the overlap-add hop and the emitted block
+ * (main.cpp:266-287: frame i lands at i * outHopSize).  out: frames * hs + (N - hs). */
+int pvr_compat_process_hs(const float* x, long n, int N, int hop_div, int hs, int frames,
+                          const float* window, int nan_faithful, double* out) {
     const int hop = N / hop_div;
     float* win = (float*)malloc(sizeof(float) * N);
     float* frame = (float*)malloc(sizeof(float) * N);
@@ -681,12 +690,12 @@ int pvr_compat_process_ex(const float* x, long n, int N, int hop_div, int frames
         pvr_compat_resynth_frame(spec, N, win, front);
         /* cudaOverlapAdd (kernel.cu:111-119): front[k-hop] += back[k], k in [hop, N);
          * then main.cpp:279 backFrame <- final_output; emit backFrame[0..hop) */
-        for (int k = hop; k < N; ++k) front[k - hop] += back[k];
-        for (int j = 0; j < hop; ++j) out[start + j] = front[j];
+        for (int k = hs; k < N; ++k) front[k - hs] += back[k];
+        for (int j = 0; j < hs; ++j) out[(long)i * hs + j] = front[j];
         memcpy(back, front, sizeof(double) * N);
     }
     /* remaining tail of the running accumulator (frames >= A carry zero spectra) */
-    for (int k = hop; k < N; ++k) out[(long)frames * hop + (k - hop)] = back[k];
+    for (int k = hs; k < N; ++k) out[(long)frames * hs + (k - hs)] = back[k];
     free(win); free(frame); free(spec); free(front); free(back);
-    return hop;
+    return hs;
 }

@@ -108,6 +108,10 @@ int pvr_compat_process(const float* x, long n, int N, int hop_div, int frames, d
  * resynthesis and the N samples of overlap-add it touches, as in the reference). */
 int pvr_compat_process_ex(const float* x, long n, int N, int hop_div, int frames,
                           const float* window, int nan_faithful, double* out);
+/* the same with the out hop hs of a time scale (phaseVocoder.h:74, phaseVocoder.cpp:68):
+ * out holds frames * hs + (N - hs) samples */
+int pvr_compat_process_hs(const float* x, long n, int N, int hop_div, int hs, int frames,
+                          const float* window, int nan_faithful, double* out);
 
 /* ---------------- fp64 helpers (exposed for tests) ---------------- */
 void pvr_fft_c64(pvr_c64* data, int L, int inverse);     /* unnormalised radix-2 DIT    */

@@ -68,6 +68,8 @@ def lib():
         L.pvr_compat_process.restype = c_int
         L.pvr_compat_process_ex.argtypes = [_f32p, c_long, c_int, c_int, c_int, ctypes.c_void_p, c_int, _f64p]
         L.pvr_compat_process_ex.restype = c_int
+        L.pvr_compat_process_hs.argtypes = [_f32p, c_long, c_int, c_int, c_int, c_int, ctypes.c_void_p, c_int, _f64p]
+        L.pvr_compat_process_hs.restype = c_int
         L.pvr_fft_c64.argtypes = [_f64p, c_int, c_int]
         L.pvr_std_process_batch.argtypes = [_f32p, c_long, c_long, c_int, c_int, c_int, c_int,
                                             c_float, c_int, _f32p, c_long, c_int]
@@ -304,15 +306,17 @@ def compat_analysis_frame(frame, N, nan_faithful=False, window=None):
     return b.view(np.complex128)  # (mag + i*phase) per bin, 2N bins
 
 
-def compat_process(x, N, hop_div, frames=None, window=None, nan_faithful=False):
+def compat_process(x, N, hop_div, frames=None, window=None, nan_faithful=False, out_hop=None):
     """REF_COMPAT whole-signal path; window: float32[N] (None = the Hamming of the
-    4-argument constructor)."""
+    4-argument constructor); out_hop: the overlap-add hop of a time scale, (int)(scale * hop)
+    (None = hop)."""
     x = _c32(x)
     hop = N // hop_div
+    hs = hop if out_hop is None else int(out_hop)
     if frames is None:
         frames = num_frames(x.shape[0], hop)
-    out = np.zeros(frames * hop + (N - hop), np.float64)
+    out = np.zeros(frames * hs + (N - hs), np.float64)
     w = None if window is None else _c32(window)
-    lib().pvr_compat_process_ex(x, x.shape[0], N, hop_div, frames,
+    lib().pvr_compat_process_hs(x, x.shape[0], N, hop_div, hs, frames,
                                 None if w is None else w.ctypes.data, 1 if nan_faithful else 0, out)
     return out

@@ -144,6 +144,23 @@ def test_ref_compat_parity(cuda, N, hop_div):
     assert err <= RMS_TOL, f"rms {err}"
 
 
+@pytest.mark.parametrize("N,hop_div,scale", [(1024, 4, 0.5), (1024, 4, 1.5), (512, 4, 0.75), (2048, 4, 2.0),
+                                          (256, 2, 0.5)])
+def test_ref_compat_time_scale_parity(cuda, N, hop_div, scale):
+    """REF_COMPAT with a time scale: the overlap-add at outHopSize = (int)(scale * hop)
+    (phaseVocoder.h:74 -> phaseVocoder.cpp:68; kernel.cu:354 keeps the spectrum unscaled),
+    against the oracle's running accumulator at that hop."""
+    x = synth(30000, 12)
+    pv = PhaseVocoder(N, TIME_SHIFT, scale, hop_div, mode=REF_COMPAT, max_frames=1000)
+    hs = pv.outHopSize
+    assert hs == int(np.float32(scale) * np.float32(N // hop_div))
+    out, _ = pv.process(to_dev(x))
+    g = out.cpu().numpy()[0]
+    ref = pvref.compat_process(x, N, hop_div, out_hop=hs)
+    assert g.shape == ref.shape
+    assert rms(g, ref) <= RMS_TOL
+
+
 def test_ref_compat_spectrum(cuda):
     N = 1024
     x = synth(N, 5)

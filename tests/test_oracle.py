@@ -360,3 +360,34 @@ def test_fp32_compat_port_pinned_to_oracle(N, hop_div):
     assert got.shape == ref.shape and used >= 1
     err = np.sqrt(np.mean((got.astype(np.float64) - ref.astype(np.float64)) ** 2, axis=1))
     assert err.max() <= 1e-6, err
+
+
+@pytest.mark.parametrize("N,hop_div,scale", [(256, 2, 0.5), (512, 4, 1.5), (1024, 4, 0.75)])
+def test_compat_out_hop_is_the_overlap_add_of_the_frames(N, hop_div, scale):
+    """REF_COMPAT with a time scale: the reference passes outHopSize = (int)(timeScale * hop)
+    to resynthesis_CUFFT (phaseVocoder.h:74, phaseVocoder.cpp:68) while cudaTimeScale's
+    factor is hard-coded 1 (kernel.cu:354), so frame i's resynthesis lands at i * outHop.
+    The oracle's running accumulator at out_hop equals the plain overlap-add of its own
+    per-frame resynthesis (pvr_compat_analysis_frame -> pvr_compat_resynth_frame), and at
+    out_hop = hop it is the unscaled path bit for bit."""
+    rng = np.random.default_rng(N + hop_div)
+    x = (0.1 * rng.standard_normal(12 * N)).astype(np.float32)
+    hop = N // hop_div
+    hs = int(np.float32(scale) * np.float32(hop))
+    frames = pvref.num_frames(len(x), hop)
+    got = pvref.compat_process(x, N, hop_div, out_hop=hs)
+    assert got.shape == (frames * hs + N - hs,)
+    L = pvref.lib()
+    w = pvref.hamming_ref(N)
+    want = np.zeros_like(got)
+    for i in range(frames):
+        fr = np.zeros(N, np.float32)
+        seg = x[i * hop:i * hop + N]
+        fr[:len(seg)] = seg
+        spec = np.empty(4 * N, np.float64)
+        L.pvr_compat_analysis_frame(fr, N, w, spec, 0)
+        y = np.empty(N, np.float64)
+        L.pvr_compat_resynth_frame(spec, N, w, y)
+        want[i * hs:i * hs + N] += y
+    assert np.max(np.abs(got - want)) <= 1e-12 * max(1.0, np.max(np.abs(want)))
+    assert np.array_equal(pvref.compat_process(x, N, hop_div, out_hop=hop), pvref.compat_process(x, N, hop_div))
