@@ -61,6 +61,33 @@ def test_pv_main_ref_compat_config1_geometry(cuda, sine440, tmp_path, batched):
     assert np.max(np.abs(s[0, :n_emit] - q)) <= 1.01 / 32768  # at most 1 LSB from rounding
 
 
+@pytest.mark.parametrize("scale", [0.5, 1.5])
+@pytest.mark.parametrize("batched", [False, True])
+def test_pv_main_ref_compat_time_scale(cuda, sine440, tmp_path, scale, batched):
+    """main.cpp's TIME_SHIFT loop at a time scale (REF_COMPAT): floor(n / outHop) frames of
+    outHop samples (main.cpp:266-287), frames past the analysed ones resynthesise zero
+    spectra; per-frame and batched drivers against the oracle's overlap-add at outHop."""
+    path, x = sine440
+    dump = str(tmp_path / "o.f32")
+    cmd = [PV_MAIN, path, "t", str(tmp_path / "o.wav"), "--N", "1024", "--hopdiv", "4",
+           "--scale", str(scale), "--dump-f32", dump]
+    if batched:
+        cmd.append("--batched")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(dump, np.float32)
+    hs = int(np.float32(scale) * np.float32(256))
+    ref = pvref.compat_process(x, 1024, 4, out_hop=hs)
+    n_emit = (len(x) // hs) * hs
+    # the batched driver dumps what it writes to the WAV (outLen = timeScale * n samples,
+    # main.cpp's output file), the per-frame one every emitted hop
+    m = min(len(got), len(ref), n_emit)
+    assert m >= min(n_emit, int(np.float32(scale) * len(x)))
+    assert rms(got[:m], ref[:m]) <= 1e-5
+    if len(got) > len(ref):
+        assert not np.any(got[len(ref):n_emit])  # past the analysed frames' overlap-add: zero spectra
+
+
 def test_pv_main_standard_batched(cuda, sine440, tmp_path):
     path, x = sine440
     dump = str(tmp_path / "o.f32")
