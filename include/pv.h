@@ -27,6 +27,9 @@
  *                      PhaseVocoder::analysis() over prev_input / prev_mag_phase /
  *                      prev_output (phaseVocoder.h:16-31; pv_analysis_RT kernel.cu:219-250;
  *                      README.md:46-50); one hipGraph replay per callback
+ *   pv_segment_*     one long stream split into consecutive frame segments, e.g. one per
+ *                      GPU (the optional time shard); no reference
+ *                      counterpart (the reference processes one stream frame by frame)
  *   pv_harmon*       the harmoniser the README plans ("multiple pitch shifts on a single
  *                      input", README.md:50): one analysis, K pitch-shift resyntheses
  *   pv_fft_c2c       FFT::HPFFT::computeGPUFFT / computeGPUIFFT (karnel/hpfft.h:6-11,
@@ -210,6 +213,26 @@ pv_status pv_analysis(pv_handle* h, const float* x, long long ldx, long long n_s
 pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
                          int frames, const float* ola_in, long long ld_ola, float* out,
                          long long ldo, void* stream);
+
+/* One long stream as consecutive non-empty frame segments s = 0, 1, ... (frames [f_s,
+ * f_s + n_s) of every channel, e.g. one segment per GPU): segment s is analysed alone
+ * (pv_analysis of x + f_s * hop), summarised (pv_segment_summary: per bin, its unwrap
+ * decisions after its first frame and its first and last phase — pv_segment_summary_words(h)
+ * int32 per channel, device memory [channels][words]), and after the summaries of segments
+ * 0 .. s - 1 are known (gathered, in order, as [s][channels][words]), resynthesised by
+ * pv_segment_resynthesis with frame0 = f_s: the unwrap counts and output phases are then those
+ * of the whole stream bit for bit (integer sums; the boundary decisions are made on the GPU
+ * with the contract's operations).  out holds the segment's own overlap-add,
+ * pv_output_length(h, n_s) samples per channel starting at stream position f_s * out_hop;
+ * its first N - out_hop samples overlap the previous segment's last ones (the caller adds
+ * them).  STANDARD handles (REF_COMPAT has no unwrap state: pv_segment_resynthesis is then
+ * pv_resynthesis).  pv_segment_summary of an empty segment is PV_ERR_ARG. */
+int pv_segment_summary_words(const pv_handle* h);
+pv_status pv_segment_summary(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                             int frames, int* summary, void* stream);
+pv_status pv_segment_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                                 int frames, long long frame0, const int* summaries, int seg, float* out,
+                                 long long ldo, void* stream);
 
 /* analysis + processing + resynthesis (spec is the caller-owned spectrum buffer).  spec may
  * be NULL when the caller does not want the spectrum: on the single launch (pv_info.

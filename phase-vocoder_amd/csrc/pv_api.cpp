@@ -159,6 +159,8 @@ struct pv_handle {
     int *d_src_first = nullptr, *d_src_cnt = nullptr;
     // workspace
     int *d_runsum = nullptr, *d_carry = nullptr;
+    int* d_seg_carry = nullptr;  // [C][bins_pad] unwrap count before a stream segment
+    float* d_seg_phi = nullptr;  // [C][bins_pad] phase of the frame before it
     float* d_tails = nullptr;
     // pv_process without a spectrum buffer on the split path: the handle's own rows
     // (max_channels x max_frames, zeroed; allocated by pv_reserve_spectrum or the first such
@@ -332,12 +334,19 @@ pv_status do_analysis(pv_handle* h, const float* x, long long ldx, long long n, 
     return PV_OK;
 }
 
+// the state before a segment of a longer stream (pv_segment_resynthesis)
+struct SegState {
+    const int* carry_in;
+    const float* phi_in;
+    unsigned t_off;
+};
+
 // carry_from: unwrap carries already scanned by another handle of the same analysis
 // geometry (the harmoniser's voices share one scan); nullptr = scan here.
 pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int C, int frames,
                          const float* ola_in, long long ld_ola, float* out, long long ldo,
                          bool have_runsum, hipStream_t s, const int* carry_from = nullptr,
-                         bool force_scan = false) {
+                         bool force_scan = false, const SegState* seg = nullptr) {
     if (C == 0 || frames == 0) {
         return PV_OK;
     }
@@ -365,6 +374,8 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
         sc.ek = h->d_ek;
         sc.runsum = h->d_runsum;
         sc.carry = h->d_carry;
+        sc.carry_in = seg ? seg->carry_in : nullptr;
+        sc.phi_in = seg ? seg->phi_in : nullptr;
         if (!have_runsum) PV_LAUNCH(h, KRS, s, pv::launch_runsum(C, sc, s));
         PV_LAUNCH(h, KC, s, pv::launch_carry(C, sc, s));
     }
@@ -401,6 +412,7 @@ pv_status do_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     p.k_lane = h->k_lane;
     p.packed = h->packed;
     p.src_hi = h->src_hi;
+    p.t_off = seg ? seg->t_off : 0u;
     const int smode = (h->mode == PV_MODE_REF_COMPAT) ? 1 : (h->pitch ? 2 : 0);
     PV_LAUNCH(h, KS, s, pv::launch_synthesis(h->L_syn, smode, C, p, s));
     const int nwg = (nruns + 3) / 4;
@@ -584,7 +596,8 @@ void pv_destroy(pv_handle* h) {
     DeviceGuard g(h->cfg.device);
     void* ptrs[] = {h->d_win, h->d_gain, h->d_ek, h->d_tw_ana, h->d_tws_ana, h->d_tw_syn,
                     h->d_tws_syn, h->d_jk_mod, h->d_src_first, h->d_src_cnt, h->d_runsum,
-                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_spec_own};
+                    h->d_carry, h->d_tails, h->d_seam_flags, h->d_spec_own, h->d_seg_carry,
+                    h->d_seg_phi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 #ifdef PV_FUSED_STAMPS
@@ -871,6 +884,8 @@ pv_status pv_create(const pv_config* cfg, pv_handle** out) {
     if (h->mode == PV_MODE_STANDARD) {
         PV_HIP(hipMalloc((void**)&h->d_runsum, sizeof(int) * runs_total * pv::kRecFields * h->bins_pad));
         PV_HIP(hipMalloc((void**)&h->d_carry, sizeof(int) * runs_total * h->bins_pad));
+        PV_HIP(hipMalloc((void**)&h->d_seg_carry, sizeof(int) * chans * h->bins_pad));
+        PV_HIP(hipMalloc((void**)&h->d_seg_phi, sizeof(float) * chans * h->bins_pad));
     }
     PV_HIP(hipMalloc((void**)&h->d_tails, sizeof(float) * wg_total * std::max(h->tail_len, 1)));
     if (h->F_fused > 0) {
@@ -909,6 +924,78 @@ pv_status pv_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec,
     ProfCall pc_(h);
     return do_resynthesis(h, spec, ld_spec, channels, frames, ola_in, ld_ola, out, ldo, false,
                           (hipStream_t)stream);
+}
+
+int pv_segment_summary_words(const pv_handle* h) {
+    return h ? pv::kSegFields * h->bins_pad : 0;
+}
+
+// run records of a spectrum (k_runsum, as pv_resynthesis makes them) -> the segment summary
+pv_status pv_segment_summary(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                             int frames, int* summary, void* stream) {
+    pv_status st = check_common(h, channels, frames);
+    if (st != PV_OK) return st;
+    if (h->mode != PV_MODE_STANDARD) return fail(PV_ERR_UNSUPPORTED, "pv_segment_summary: STANDARD handles only");
+    if (channels == 0) return PV_OK;
+    if (!summary) return fail(PV_ERR_ARG, "null summary");
+    // (an empty segment has no first or last phase: the caller leaves it out of the order)
+    if (frames == 0) return fail(PV_ERR_ARG, "pv_segment_summary: empty segment");
+    if (!spec) return fail(PV_ERR_ARG, "null spec");
+    if (ld_spec < (long long)frames * h->spec_stride) return fail(PV_ERR_ARG, "ld_spec < frames * spec_stride");
+    DeviceGuard g(h->cfg.device);
+    ProfCall pc_(h);
+    hipStream_t s = (hipStream_t)stream;
+    pv::ScanParams sc{};
+    sc.spec = reinterpret_cast<const float2*>(spec);
+    sc.ld_spec = ld_spec;
+    sc.spec_stride = h->spec_stride;
+    sc.frames = frames;
+    sc.F = h->F;
+    sc.nruns = nruns_of(h, frames);
+    sc.L = h->L_syn;
+    sc.bins_pad = h->bins_pad;
+    sc.packed = h->packed;
+    sc.ek = h->d_ek;
+    sc.runsum = h->d_runsum;
+    PV_LAUNCH(h, KRS, s, pv::launch_runsum(channels, sc, s));
+    pv::SegParams sp{};
+    sp.runsum = h->d_runsum;
+    sp.nruns = sc.nruns;
+    sp.L = h->L_syn;
+    sp.bins_pad = h->bins_pad;
+    sp.channels = channels;
+    sp.ek = h->d_ek;
+    sp.summary = summary;
+    PV_LAUNCH(h, KRS, s, pv::launch_segsum(sp, s));
+    return PV_OK;
+}
+
+pv_status pv_segment_resynthesis(pv_handle* h, const pv_float2* spec, long long ld_spec, int channels,
+                                 int frames, long long frame0, const int* summaries, int seg, float* out,
+                                 long long ldo, void* stream) {
+    pv_status st = check_common(h, channels, frames);
+    if (st != PV_OK) return st;
+    if (frame0 < 0 || seg < 0) return fail(PV_ERR_ARG, "negative frame0 / seg");
+    if (seg > 0 && !summaries) return fail(PV_ERR_ARG, "null summaries");
+    if (channels == 0 || frames == 0) return PV_OK;
+    DeviceGuard g(h->cfg.device);
+    ProfCall pc_(h);
+    hipStream_t s = (hipStream_t)stream;
+    if (h->mode != PV_MODE_STANDARD)  // no unwrap state: the segment is a plain resynthesis
+        return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, false, s);
+    pv::SegParams sp{};
+    sp.L = h->L_syn;
+    sp.bins_pad = h->bins_pad;
+    sp.channels = channels;
+    sp.ek = h->d_ek;
+    sp.summaries = summaries;
+    sp.seg = seg;
+    sp.carry_in = h->d_seg_carry;
+    sp.phi_in = h->d_seg_phi;
+    PV_LAUNCH(h, KC, s, pv::launch_segcarry(sp, s));
+    const SegState ss{h->d_seg_carry, h->d_seg_phi, (unsigned)((unsigned long long)frame0 % h->q)};
+    return do_resynthesis(h, spec, ld_spec, channels, frames, nullptr, 0, out, ldo, false, s, nullptr,
+                          /*force_scan*/ false, &ss);
 }
 
 // the handle's own spectrum rows (split path, pv_process with spec = NULL): allocated and

@@ -53,6 +53,25 @@ struct ScanParams {
     const float* ek;
     int* runsum;
     int* carry;
+    // a segment of a longer stream (pv_segment_resynthesis), or nullptr: the unwrap count
+    // before the segment's first frame and the phase of the frame before it, [C][bins_pad]
+    const int* carry_in;
+    const float* phi_in;
+};
+
+// per-segment summaries of a stream split into consecutive frame segments
+// (pv_segment_summary / pv_segment_resynthesis): [seg][C][kSegFields][bins_pad] int32 —
+// the segment's unwrap decisions after its first frame, phi of its first and of its last frame
+constexpr int kSegFields = 3;
+struct SegParams {
+    const int* runsum;                 // the segment's run records (k_runsum)
+    int nruns, L, bins_pad, channels;
+    const float* ek;
+    int* summary;                      // k_segsum: this segment's [C][kSegFields][bins_pad]
+    const int* summaries;              // k_segcarry: the earlier segments' summaries
+    int seg;                           // k_segcarry: how many segments come before this one
+    int* carry_in;                     // k_segcarry outputs, [C][bins_pad]
+    float* phi_in;
 };
 
 struct SynParams {
@@ -83,6 +102,8 @@ struct SynParams {
     int packed;                        // PV_SPEC_PACKED rows (bins 0 and L in slot 0)
     int src_hi;                        // highest analysis bin an output bin reads (single-
                                        // source pitch: the row slots above it are not read)
+    unsigned t_off;                    // (index of the first frame in the whole stream) mod q:
+                                       // 0 unless a segment of a longer stream
 };
 
 // single-launch STANDARD path for q = 1 (pv_fused.hip)
@@ -179,6 +200,8 @@ int std_analysis_wgs_per_cu(int L, int hop, bool ek_lane, bool packed, int* wave
 hipError_t launch_compat_analysis(int L, int channels, const AnaParams& p, hipStream_t s);
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s);
 hipError_t launch_carry(int channels, const ScanParams& p, hipStream_t s);
+hipError_t launch_segsum(const SegParams& p, hipStream_t s);
+hipError_t launch_segcarry(const SegParams& p, hipStream_t s);
 hipError_t launch_synthesis(int L, int mode, int channels, const SynParams& p, hipStream_t s);
 // the synthesis kernel for this geometry can take SynParams.k_lane (register overlap-add,
 // power-of-two q, STANDARD)

@@ -73,11 +73,13 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
     auto S_of = [&](int r) { return rs[(long long)r * RF * BP]; };
     auto first_of = [&](int r) { return __int_as_float(rs[(long long)r * RF * BP + BP]); };
     auto last_of = [&](int r) { return __int_as_float(rs[(long long)r * RF * BP + 2 * BP]); };
+    // phi(-1) = 0 and M = 0 before the stream, or a longer stream's state before this segment
+    const float phi0 = (p.phi_in && on) ? p.phi_in[(long long)c * BP + k] : 0.0f;
     int M = 0;
     int run = r0;
     if constexpr (SEG > 1) {  // pass 1 only feeds the other segments' offsets
         int T = 0;
-        float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : 0.0f;
+        float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : phi0;
         for (; run + 4 <= r1; run += 4) {
             int sv[4];
             float fv[4], lv[4];
@@ -102,8 +104,9 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
         for (int j = 0; j < sg; ++j) M += tot[j][lane];
     }
     if (!on) return;
+    if (p.carry_in) M += p.carry_in[(long long)c * BP + k];
     run = r0;
-    float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : 0.0f;
+    float prev = (r0 > 0 && r0 < r1) ? last_of(r0 - 1) : phi0;
     for (; run + 4 <= r1; run += 4) {
         int sv[4];
         float fv[4], lv[4];
@@ -127,6 +130,57 @@ __global__ __launch_bounds__(64 * SEG) void k_carry(ScanParams p) {
         M += S_of(run);
         prev = last_of(run);
     }
+}
+
+// ------------------------------------------------------------------ stream segments
+// A stream cut into consecutive frame segments (one per rank, pv_segment_*): the unwrap count
+// is an integer sum, so a segment's carries need only, per bin, the earlier segments' decision
+// totals and their boundary phases — the decisions at the segment boundaries are made here
+// with the same operations as everywhere else (unwrap_count), so the carries equal the whole
+// stream's bit for bit.
+// k_segsum: T = the decisions of the segment's frames after its first (run 0's S, then each
+// later run's first decision against the previous run's last phase plus its S), phi(first),
+// phi(last).
+__global__ __launch_bounds__(256) void k_segsum(SegParams p) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (k > p.L) return;
+    const int BP = p.bins_pad;
+    constexpr int RF = kRecFields;
+    const int* rs = p.runsum + (long long)c * p.nruns * RF * BP + k;
+    const float e = p.ek[k];
+    int T = rs[0];
+    float prev = __int_as_float(rs[2 * BP]);
+    for (int r = 1; r < p.nruns; ++r) {
+        const int* rr = rs + (long long)r * RF * BP;
+        T += unwrap_count(__int_as_float(rr[BP]), prev, e) + rr[0];
+        prev = __int_as_float(rr[2 * BP]);
+    }
+    int* dst = p.summary + (long long)c * kSegFields * BP + k;
+    dst[0] = T;
+    dst[BP] = rs[BP];
+    dst[2 * BP] = __float_as_int(prev);
+}
+
+// k_segcarry: the state before segment `seg` from the summaries of segments 0 .. seg - 1:
+// M = sum over j of (m(first_j) against last_{j-1}, last_{-1} = 0) + T_j; phi_in = last_{seg-1}
+__global__ __launch_bounds__(256) void k_segcarry(SegParams p) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (k >= p.bins_pad) return;
+    const int BP = p.bins_pad;
+    int M = 0;
+    float prev = 0.0f;
+    if (k <= p.L) {
+        const float e = p.ek[k];
+        for (int j = 0; j < p.seg; ++j) {
+            const int* sj = p.summaries + ((long long)j * p.channels + c) * kSegFields * BP + k;
+            M += unwrap_count(__int_as_float(sj[BP]), prev, e) + sj[0];
+            prev = __int_as_float(sj[2 * BP]);
+        }
+    }
+    p.carry_in[(long long)c * BP + k] = M;
+    p.phi_in[(long long)c * BP + k] = prev;
 }
 
 // ------------------------------------------------------------------ K3 synthesis
@@ -407,6 +461,16 @@ size_t synthesis_lds_bytes(int L, int hs) {
 hipError_t launch_runsum(int channels, const ScanParams& p, hipStream_t s) {
     dim3 grid((p.L + 1 + 255) / 256, p.nruns, channels);
     hipLaunchKernelGGL(k_runsum, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_segsum(const SegParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_segsum, dim3((p.L + 1 + 255) / 256, p.channels), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_segcarry(const SegParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_segcarry, dim3((p.bins_pad + 255) / 256, p.channels), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

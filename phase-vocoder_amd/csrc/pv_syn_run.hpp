@@ -314,7 +314,8 @@ __device__ __forceinline__ void syn_run(const SynParams& p, const SynCarve& sc, 
     }
     const unsigned q32 = (unsigned)p.q;  // <= 2^24 (QPOW2) or <= 32768
     auto synth = [&](int u, int t, const float2 (&sv)[E + 1], float2 (&z)[E], const auto& hk) {
-        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) & (q32 - 1u)) : ((unsigned)(t + 1) % q32);
+        // (t_off: a segment's first frame index in its whole stream, mod q)
+        const unsigned tq = QPOW2 ? ((unsigned)(t + 1) + p.t_off) & (q32 - 1u) : ((unsigned)(t + 1) + p.t_off) % q32;
         using H = std::decay_t<decltype(hk)>;
         // (L = 1024: the radix-16/16/4 inverse FFT on the v3 pass table, p.tw)
         synth_frame<L, MODE, !ROLA, QPOW2, KREG, RACC, false, H, TwS, (L == 1024)>(

@@ -118,6 +118,12 @@ def lib():
     L.pv_analysis.restype = i
     L.pv_resynthesis.argtypes = [vp, vp, ll, i, i, vp, ll, vp, ll, vp]
     L.pv_resynthesis.restype = i
+    L.pv_segment_summary_words.argtypes = [vp]
+    L.pv_segment_summary_words.restype = i
+    L.pv_segment_summary.argtypes = [vp, vp, ll, i, i, vp, vp]
+    L.pv_segment_summary.restype = i
+    L.pv_segment_resynthesis.argtypes = [vp, vp, ll, i, i, ll, vp, i, vp, ll, vp]
+    L.pv_segment_resynthesis.restype = i
     L.pv_process.argtypes = [vp, vp, ll, ll, i, i, vp, ll, vp, ll, vp]
     L.pv_process.restype = i
     L.pv_reserve_spectrum.argtypes = [vp]

@@ -52,3 +52,72 @@ def broadcast_tables(pv, src: int = 0, group=None, local=None):
     if ref is None:
         return None
     return bool(torch.equal(blob, ref.export_tables()))
+
+
+# ---------------------------------------------------------------- one stream, many ranks
+# SURVEY.md §8(e), the optional time shard: a single long stream split into consecutive frame
+# segments, one per rank.  The frames are independent; the only sequential quantity is the
+# per-bin integer unwrap count, so each rank summarises its segment (pv_segment_summary: a
+# decision total and two boundary phases per bin), the summaries are all-gathered (one
+# collective of C x 3 x bins_pad int32 per rank), and each rank resynthesises its segment
+# with the count of everything before it (pv_segment_resynthesis) — the same unwrap counts
+# and output phases as one GPU processing the whole stream.  The overlap of neighbouring
+# segments' outputs (N - out_hop samples) is added where the blocks are assembled.
+
+def frame_segments(total_frames: int, world: int) -> list[tuple[int, int]]:
+    """Consecutive frame segments (first, count) for ranks 0 .. world - 1; sizes differ by
+    <= 1 and empty segments (world > total_frames) come last."""
+    return [channel_shard(total_frames, world, r) for r in range(world)]
+
+
+def assemble_segments(blocks, firsts, out_hop: int, out_len: int):
+    """Sum each segment's overlap-add block at its stream position first * out_hop (numpy or
+    torch, [C, len] each) -> the whole stream's output [C, out_len]."""
+    import numpy as np
+    is_np = isinstance(blocks[0], np.ndarray)
+    if is_np:
+        out = np.zeros((blocks[0].shape[0], out_len), blocks[0].dtype)
+    else:
+        import torch
+        out = torch.zeros((blocks[0].shape[0], out_len), dtype=blocks[0].dtype, device=blocks[0].device)
+    for b, f in zip(blocks, firsts):
+        p = f * out_hop
+        n = min(b.shape[1], out_len - p)
+        if n > 0:
+            out[:, p:p + n] += b[:, :n]
+    return out
+
+
+def process_stream_segments(pv, x, group=None, n_samples: int | None = None):
+    """Run one stream [C, n] (on this rank's device; every rank holds it, or at least its
+    own frames' samples at their stream positions) as this rank's frame segment.  Returns
+    (block, first_frame, segments): this rank's overlap-add block [C, frames*outHop + N -
+    outHop] (None for an empty segment) and the (first, count) list of all ranks."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    x = x.unsqueeze(0) if x.dim() == 1 else x
+    C, n = x.shape
+    n = n if n_samples is None else n_samples
+    total = pv.num_frames(n)
+    segs = frame_segments(total, world)
+    f0, nf = segs[rank]
+    hop = pv.hopSize
+    words = pv._L.pv_segment_summary_words(pv._h)
+    spec = None
+    if nf > 0:
+        spec = pv.analysis(x[:, f0 * hop:], frames=nf, n_samples=n - f0 * hop)
+        mine = pv.segment_summary(spec, nf)
+    else:
+        mine = torch.zeros((C, words), dtype=torch.int32, device=x.device)
+    nccl = dist.get_backend(group) == "nccl"
+    send = mine if nccl else mine.cpu()
+    got = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(got, send, group=group)
+    if nf == 0:
+        return None, f0, segs
+    # the earlier non-empty segments, in stream order (empty ones come last: none precedes)
+    before = [got[j] for j in range(rank) if segs[j][1] > 0]
+    summaries = torch.stack(before).to(x.device).contiguous() if before else None
+    block = pv.segment_resynthesis(spec, f0, summaries, frames=nf)
+    return block, f0, segs

@@ -200,6 +200,37 @@ class PhaseVocoder:
                                           self._stream(stream)), "pv_resynthesis")
         return out
 
+    # -------------------------------------------------------------- stream segments
+    def segment_summary(self, spec, frames: int | None = None, stream=None):
+        """pv_segment_summary: spec [C, frames, spec_stride, 2] of one segment of a longer
+        stream -> summary [C, words] int32 (device)."""
+        torch = _torch()
+        C = spec.shape[0]
+        frames = spec.shape[1] if frames is None else frames
+        words = self._L.pv_segment_summary_words(self._h)
+        summary = torch.empty((C, words), dtype=torch.int32, device=spec.device)
+        self._call(self._L.pv_segment_summary(self._h, _ptr(spec), spec.stride(0) // 2, C, frames,
+                                              _ptr(summary), self._stream(stream)), "pv_segment_summary")
+        return summary
+
+    def segment_resynthesis(self, spec, frame0: int, summaries=None, frames: int | None = None, out=None,
+                            stream=None):
+        """pv_segment_resynthesis: the segment starting at stream frame `frame0`, after the
+        earlier segments' summaries [s, C, words] (None or empty for the first segment) ->
+        its own overlap-add [C, frames*outHop + N - outHop]."""
+        C = spec.shape[0]
+        frames = spec.shape[1] if frames is None else frames
+        if out is None:
+            out = self.alloc_out(C, frames)
+        seg = 0 if summaries is None else int(summaries.shape[0])
+        if seg:
+            assert summaries.is_contiguous() and summaries.dtype == _torch().int32
+        self._call(self._L.pv_segment_resynthesis(self._h, _ptr(spec), spec.stride(0) // 2, C, frames,
+                                                  int(frame0), _ptr(summaries) if seg else None, seg,
+                                                  _ptr(out), out.stride(0), self._stream(stream)),
+                   "pv_segment_resynthesis")
+        return out
+
     def process(self, x, frames: int | None = None, n_samples: int | None = None, spec=None,
                 out=None, stream=None, spectrum: bool = True):
         """analysis -> processing -> resynthesis; returns (out, spec).  spectrum=False: the

@@ -111,3 +111,51 @@ def test_broadcast_tables_gloo():
         assert results[r][2:] == results[0][2:]
     assert results[1][0] is None       # nothing local to compare with
     assert results[2][0] is True       # its local build (seed 99) equals rank 0's
+
+
+def test_frame_segments_cover_the_stream_in_order():
+    from pvamd.dist import frame_segments
+    for total in (0, 1, 3, 10, 1722, 10335):
+        for world in (1, 2, 3, 8):
+            segs = frame_segments(total, world)
+            assert len(segs) == world
+            pos = 0
+            for f, c in segs:
+                assert f == pos and c >= 0
+                pos += c
+            assert pos == total
+            counts = [c for _, c in segs]
+            assert max(counts) - min(counts) <= 1
+            # empty segments only at the end (pv_segment_summary refuses an empty one)
+            assert counts == sorted(counts, reverse=True)
+
+
+def test_assemble_segments_is_the_overlap_add_of_the_blocks():
+    import numpy as np
+    from pvamd.dist import assemble_segments, frame_segments
+    rng = np.random.default_rng(5)
+    N, hs, total, C = 64, 16, 37, 2
+    frames = rng.standard_normal((C, total, N))
+    want = np.zeros((C, total * hs + N - hs))
+    for t in range(total):
+        want[:, t * hs:t * hs + N] += frames[:, t]
+    blocks, firsts = [], []
+    for f, c in frame_segments(total, 3):
+        b = np.zeros((C, c * hs + N - hs))
+        for u in range(c):
+            b[:, u * hs:u * hs + N] += frames[:, f + u]
+        blocks.append(b)
+        firsts.append(f)
+    got = assemble_segments(blocks, firsts, hs, want.shape[1])
+    assert np.allclose(got, want, rtol=0, atol=1e-12)
+
+
+def test_segment_abi_checks_without_gpu():
+    import ctypes
+    from pvamd import _lib
+    L = _lib.lib()
+    assert L.pv_segment_summary_words(None) == 0
+    assert L.pv_segment_summary(None, None, 0, 1, 1, None, None) == _lib.PV_ERR_ARG
+    assert L.pv_segment_resynthesis(None, None, 0, 1, 1, 0, None, 0, None, 0, None) == _lib.PV_ERR_ARG
+    assert {"pv_segment_summary", "pv_segment_resynthesis", "pv_segment_summary_words"} <= set(_lib.declared_symbols())
+    del ctypes
