@@ -1,4 +1,5 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_segments.py -m gpu -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_new.log 2>&1; rc=$?
-tail -40 gpurun_out/pytest_new.log; exit $rc
+echo "# c3" && AB_STEPS=20 bash scripts/ab.sh notoff || exit $?
+echo "# c4" && AB_STEPS=20 AB_ARGS="--workload c4" bash scripts/ab.sh notoff || exit $?
+echo all done
