@@ -49,6 +49,11 @@
  *   PV_FUSED_BALANCE=0   single launch of one channel: uniform runs (no balanced F+1 runs)
  *   PV_COMPAT_ANA_FRAMES=F  REF_COMPAT analysis run length (1..256, default 4)
  *   PV_RT_LAUNCH=direct  pv_rt_callback launches the kernel instead of replaying the graph
+ *
+ * Concurrency: a handle's compute calls share its workspace (run records, carries, seam
+ * tails, segment state), so the calls on one handle must be ordered — one stream, or
+ * streams synchronised between calls; different handles are independent.  pv_last_error
+ * is per thread; pv_reserve_spectrum is thread-safe.
  */
 #ifndef PV_H
 #define PV_H
@@ -66,7 +71,9 @@ extern "C" {
                                 misread struct), pv_config.spec_layout, the chained path
                                 and pv_check_device removed;
                              5: pv_config.tables_external, pv_process(spec = NULL) on the
-                                single launch */
+                                single launch (later additions are functions only, no
+                                struct change: pv_sources_sha, pv_reserve_spectrum,
+                                pv_segment_*) */
 
 typedef struct pv_handle pv_handle;
 
