@@ -1,5 +1,6 @@
 set -u
 mkdir -p gpurun_out
-echo "# c3" && AB_STEPS=20 bash scripts/ab.sh notoff || exit $?
-echo "# c4" && AB_STEPS=20 AB_ARGS="--workload c4" bash scripts/ab.sh notoff || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+STEPS="tests c3 c2 c4 compat rt prof prof_c4 prof_c2 prof_compat" bash scripts/round_evidence.sh || exit $?
 echo all done
