@@ -1,6 +1,4 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-STEPS="tests c3 c2 c4 compat rt prof prof_c4 prof_c2 prof_compat" bash scripts/round_evidence.sh || exit $?
-echo all done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rf --timeout 120 --timeout-method thread -k "capacity or two_handles" > gpurun_out/pytest_new.log 2>&1; rc=$?
+tail -30 gpurun_out/pytest_new.log; exit $rc

@@ -459,3 +459,51 @@ def test_reserve_spectrum_on_single_launch_is_a_no_op(cuda):
     assert spec is None
     ref = pvref.std_process(synth(30000, 6), 1024, 4, ord("p"), 2.0)
     assert rms(out.cpu().numpy()[0], ref) <= RMS_TOL
+
+
+def test_capacity_limits_are_enforced_and_reachable(cuda):
+    """A call may use exactly the handle's max_channels x max_frames (every kernel grid and
+    workspace sized for it) and is refused beyond either, before any launch."""
+    import torch
+    from pvamd import _lib
+    N, hop = 1024, 256
+    C, F = 3, 40
+    n = (F + 1) * hop  # exactly F frames (main.cpp:231)
+    pv = PhaseVocoder(N, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_channels=C, max_frames=F)
+    assert pv.num_frames(n) == F
+    xs = np.stack([synth(n, 40 + c) for c in range(C)])
+    out, _ = pv.process(torch.from_numpy(xs).cuda())
+    ref, _ = pvref.std_process_batch(xs, N, 4, ord("t"), 0.5)
+    for c in range(C):
+        assert rms(out.cpu().numpy()[c], ref[c]) <= RMS_TOL
+    with pytest.raises(_lib.PVError, match="capacity"):
+        pv.process(torch.from_numpy(np.stack([synth(n + hop, 1)] * C)).cuda())  # F + 1 frames
+    with pytest.raises(_lib.PVError, match="capacity"):
+        pv.process(torch.from_numpy(np.stack([synth(n, 1)] * (C + 1))).cuda())  # C + 1 channels
+    # the handle still works after the refusals
+    out2, _ = pv.process(torch.from_numpy(xs).cuda())
+    assert torch.equal(out, out2)
+
+
+def test_two_handles_on_two_streams_are_independent(cuda):
+    """include/pv.h: different handles share nothing — two handles driven concurrently on two
+    streams give the same bits as each alone."""
+    import torch
+    xs = np.stack([synth(50000, 60 + c) for c in range(2)])
+    xd = torch.from_numpy(xs).cuda()
+    a = PhaseVocoder(1024, TIME_SHIFT, 0.5, 4, mode=STANDARD, max_channels=2, max_frames=300)
+    b = PhaseVocoder(2048, PITCH_SHIFT, 1.5, 4, mode=STANDARD, max_channels=2, max_frames=300)
+    ra, _ = a.process(xd)
+    rb, _ = b.process(xd)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(3):
+        oa, ob = a.alloc_out(2, a.num_frames(50000)), b.alloc_out(2, b.num_frames(50000))
+        a.process(xd, out=oa, spectrum=False, stream=s1.cuda_stream)
+        b.process(xd, out=ob, spectrum=False, stream=s2.cuda_stream)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    for oa, ob in outs:
+        assert torch.equal(oa, ra) and torch.equal(ob, rb)
