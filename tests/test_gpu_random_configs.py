@@ -74,3 +74,33 @@ def test_random_configuration_in_segments(cuda, seed):
     got = run_segments(pv, xd, nseg)
     assert got.shape == whole.shape
     assert np.max(np.abs(got.cpu().numpy() - whole.cpu().numpy())) <= 1e-6, (seed, N, hop_div, effect, scale)
+
+
+@pytest.mark.parametrize("seed", list(range(16)))
+def test_random_real_time_configuration(cuda, seed):
+    """Real-time mode (pv_rt_*) on random draws: the stream pushed in random-size blocks of
+    whole hops equals the oracle's offline pipeline over the zero-prefixed stream."""
+    from pvamd import RealTimeVocoder
+    from test_gpu_rt import dev, oracle_stream
+    rng = np.random.default_rng(9000 + seed)
+    N = int(rng.choice([256, 512, 1024, 2048]))
+    hop_div = int(rng.choice([2, 4, 4, 8]))
+    if rng.random() < 0.5:
+        effect, scale = PITCH_SHIFT, float(rng.choice([0.75, 1.0, 1.5, 2.0]))
+    else:
+        effect, scale = TIME_SHIFT, float(rng.choice([0.5, 0.75, 1.0, 1.5]))
+    hop = N // hop_div
+    K = int(rng.integers(6, 40))
+    x = synth(K * hop, 9500 + seed)
+    rt = RealTimeVocoder(N, effect, scale, hop_div, channels=1)
+    hs = rt.outHopSize
+    xd = dev(x)
+    outs, j = [], 0
+    while j < K:
+        m = int(min(K - j, rng.integers(1, 5)))
+        outs.append(rt.push(xd[j * hop:(j + m) * hop]).cpu().numpy()[0])
+        j += m
+    g = np.concatenate(outs)
+    assert g.shape == (K * hs,)
+    _, ref = oracle_stream(x, N, hop_div, effect, scale, K)
+    assert rms(g, ref[:K * hs]) <= RMS_TOL, (seed, N, hop_div, effect, scale, K)
